@@ -1,0 +1,190 @@
+/*
+ * migmres.h -- C ABI of the MI355X-native Block GMRES hot path.
+ *
+ * This is the drop-in boundary between a Belos driver (Belos::MultiVecTraits /
+ * Belos::OperatorTraits / Belos::SolverManager, or the Python mirror in
+ * trilinos_amd/) and the HIP kernels.  Every entry point is plain C: opaque
+ * handles, raw pointers, sizes; no torch or C++ types cross it.
+ *
+ * Reference interfaces each group replaces (paths under /root/reference/packages):
+ *   context      Epetra_Comm / Epetra_MpiComm::SumAll        epetra/src/Epetra_MpiComm.cpp:123-127
+ *   map          Epetra_BlockMap::ConstructAutoUniform        epetra/src/Epetra_BlockMap.cpp:60-107
+ *   crs          Epetra_CrsMatrix::FillComplete/Multiply      epetra/src/Epetra_CrsMatrix.cpp:1147-1199, 3107-3285
+ *                Epetra_CrsGraph::MakeColMap_int              epetra/src/Epetra_CrsGraph.cpp:1348-1524
+ *                Epetra_Import::Construct                     epetra/src/Epetra_Import.cpp:292-460
+ *                Tpetra::CrsMatrix::apply                     tpetra/core/src/Tpetra_CrsMatrix_def.hpp:5176-5208
+ *   mv           Belos::MultiVecTraits<double,Epetra_MultiVector>
+ *                                                             belos/epetra/src/BelosEpetraAdapter.hpp:447-1064
+ *   icgs         Belos::ICGSOrthoManager::projectAndNormalize / normalize
+ *                                                             belos/src/BelosICGSOrthoManager.hpp:646-839
+ *   solver       Belos::BlockGmresSolMgr (setParameters/solve/getNumIters/achievedTol/isLOADetected)
+ *                                                             belos/src/BelosBlockGmresSolMgr.hpp:494-803, 916-1303
+ *
+ * Conventions
+ *   - Return 0 on success, a negative code on error (Epetra's EPETRA_CHK_ERR style);
+ *     migmres_last_error() returns a thread-local message for the last failure.
+ *   - Dense coefficient matrices cross the ABI as host, column-major arrays with a
+ *     leading dimension (Teuchos::SerialDenseMatrix layout).
+ *   - Calls that return host data (transmv, dot, norm, icgs rank, solve) block until the
+ *     device work and any cross-GPU reduction finished; others are stream-ordered.
+ *   - A context is not thread-safe (Belos is single-threaded per rank).
+ */
+#ifndef MIGMRES_H
+#define MIGMRES_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MIGMRES_ABI_VERSION 1
+
+typedef struct migmres_ctx migmres_ctx;
+typedef struct migmres_crs migmres_crs;
+typedef struct migmres_mv migmres_mv;
+typedef struct migmres_solver migmres_solver;
+
+/* error codes */
+#define MIGMRES_OK 0
+#define MIGMRES_EINVAL -1
+#define MIGMRES_EHIP -2
+#define MIGMRES_ERCCL -3
+#define MIGMRES_ENOMEM -4
+#define MIGMRES_ESTATE -5
+
+/* norm types (Belos::NormType, belos/src/BelosTypes.hpp) */
+#define MIGMRES_ONE_NORM 0
+#define MIGMRES_TWO_NORM 1
+#define MIGMRES_INF_NORM 2
+
+int migmres_abi_version(void);
+const char *migmres_last_error(void);
+
+/* ---------------- context (replaces Epetra_Comm + the MPI backend) ---------------- */
+
+/* 128-byte RCCL unique id, generated on rank 0 and broadcast by the caller. */
+int migmres_comm_unique_id(unsigned char out[128]);
+/* nranks == 1: uid may be NULL and no communicator is created. */
+int migmres_ctx_create(int device, int rank, int nranks, const unsigned char *uid, migmres_ctx **out);
+int migmres_ctx_destroy(migmres_ctx *ctx);
+int migmres_ctx_sync(migmres_ctx *ctx);
+int migmres_ctx_rank(const migmres_ctx *ctx, int *rank, int *nranks);
+/* Sum-all of n host doubles across ranks (Epetra_Comm::SumAll). */
+int migmres_ctx_sum_all(migmres_ctx *ctx, const double *in, double *out, int n);
+
+/* ---------------- maps and import plans (host only, no GPU needed) ---------------- */
+
+/* Epetra_BlockMap::ConstructAutoUniform: first global id and local length of `rank`. */
+int migmres_map_uniform(long long n_global, int nranks, int rank, long long *first, int *n_local);
+
+/* Epetra_CrsGraph::MakeColMap_int for one rank.  rowptr[n_local+1], gcols in insertion
+ * order.  colmap_out must hold n_local + (number of distinct remote columns) entries;
+ * *n_cols returns the count.  Pass colmap_out == NULL to query the size. */
+int migmres_plan_colmap(long long n_global, int nranks, long long first, int n_local,
+                        const long long *rowptr, const long long *gcols,
+                        long long *colmap_out, int *n_cols);
+
+/* Remote part of Epetra_Import::Construct for one rank: given the column map, the
+ * remote LIDs / GIDs / owner PIDs sorted by PID (Epetra_Util::Sort). Arrays sized
+ * n_cols; *n_remote and *num_same returned. */
+int migmres_plan_remotes(long long n_global, int nranks, long long first, int n_local,
+                         const long long *colmap, int n_cols, int *num_same,
+                         int *remote_lids, long long *remote_gids, int *remote_pids, int *n_remote);
+
+/* Local CRS after MakeIndicesLocal + SortEntries: lcols/vals out sized rowptr[n_local]. */
+int migmres_plan_local_crs(long long first, int n_local, const long long *rowptr,
+                           const long long *gcols, const double *vals, const long long *colmap,
+                           int n_cols, int *lcols_out, double *vals_out);
+
+/* ---------------- CRS operator (Epetra_CrsMatrix / Tpetra::CrsMatrix) ---------------- */
+
+/* Collective over the context's ranks: builds the column map, local indices, the
+ * import plan (exchanging remote-id lists) and uploads the operator. */
+int migmres_crs_create(migmres_ctx *ctx, long long n_global, long long first, int n_local,
+                       const long long *rowptr, const long long *gcols, const double *vals,
+                       migmres_crs **out);
+/* Galeri generators built natively on the host of each rank ("Laplace2D",
+ * "Laplace3D"); nz ignored for 2-D. */
+int migmres_crs_create_galeri(migmres_ctx *ctx, const char *kind, int nx, int ny, int nz,
+                              migmres_crs **out);
+int migmres_crs_destroy(migmres_crs *A);
+int migmres_crs_info(const migmres_crs *A, long long *n_global, long long *first, int *n_local,
+                     int *n_cols, long long *nnz_local, int *n_remote, int *n_export);
+int migmres_crs_colmap(const migmres_crs *A, long long *colmap_out);
+/* Export list (ExportLIDs, ExportPIDs) and remote list (RemoteLIDs) of the import plan. */
+int migmres_crs_import_plan(const migmres_crs *A, int *export_lids, int *export_pids,
+                            int *remote_lids, int *remote_pids);
+/* OperatorTraits::Apply / Tpetra apply: Y = alpha*A*X + beta*Y (beta==0 ignores Y). */
+int migmres_crs_apply(migmres_crs *A, const migmres_mv *X, migmres_mv *Y, double alpha, double beta);
+
+/* ---------------- multivectors (Belos::MultiVecTraits) ---------------- */
+
+/* Owned N_local x ncols block (uninitialised contents, MVT::Clone). */
+int migmres_mv_create(migmres_ctx *ctx, long long n_global, int n_local, int ncols, migmres_mv **out);
+/* MVT::CloneView(NonConst): a non-owning view of columns idx[0..n-1] of parent. */
+int migmres_mv_view(migmres_mv *parent, const int *idx, int n, migmres_mv **out);
+/* MVT::CloneView with a contiguous Range1D [first, first+n). */
+int migmres_mv_view_range(migmres_mv *parent, int first, int n, migmres_mv **out);
+int migmres_mv_destroy(migmres_mv *mv);
+int migmres_mv_shape(const migmres_mv *mv, long long *n_global, int *n_local, int *ncols,
+                     int *constant_stride);
+/* Host <-> device copies of the local rows (column-major host array, leading dim ld). */
+int migmres_mv_upload(migmres_mv *mv, const double *host, long long ld);
+int migmres_mv_download(const migmres_mv *mv, double *host, long long ld);
+
+/* mv = beta*mv + alpha*A*B, B (A.ncols x mv.ncols) host column-major (MvTimesMatAddMv). */
+int migmres_mv_times_mat_add_mv(double alpha, const migmres_mv *A, const double *B, int ldb,
+                                double beta, migmres_mv *mv);
+/* mv = alpha*A + beta*B (MvAddMv). */
+int migmres_mv_add_mv(double alpha, const migmres_mv *A, double beta, const migmres_mv *B,
+                      migmres_mv *mv);
+int migmres_mv_scale(migmres_mv *mv, double alpha);                 /* MvScale(scalar) */
+int migmres_mv_scale_vec(migmres_mv *mv, const double *alphas);     /* MvScale(vector) */
+/* C (A.ncols x B.ncols, host, ldc) = alpha * A^T B, summed over all ranks (MvTransMv). */
+int migmres_mv_trans_mv(double alpha, const migmres_mv *A, const migmres_mv *B, double *C, int ldc);
+int migmres_mv_dot(const migmres_mv *A, const migmres_mv *B, double *out);   /* MvDot */
+int migmres_mv_norm(const migmres_mv *mv, double *out, int norm_type);       /* MvNorm */
+int migmres_mv_init(migmres_mv *mv, double alpha);                           /* MvInit */
+/* MvRandom with Epetra_MultiVector::Random semantics: column-major MINSTD stream from
+ * *seed over the GLOBAL rows (partition independent); *seed is advanced. */
+int migmres_mv_random(migmres_mv *mv, unsigned int *seed);
+int migmres_mv_assign(const migmres_mv *A, migmres_mv *mv);                  /* Assign */
+int migmres_mv_set_block(const migmres_mv *A, const int *idx, int n, migmres_mv *mv); /* SetBlock */
+
+/* ---------------- ICGS orthogonalisation (Belos::ICGSOrthoManager) ---------------- */
+
+/* projectAndNormalize(X, [C], B, [Q]): C (Q.ncols x X.ncols, ldc), B (X.ncols^2, ldb). */
+int migmres_icgs_project_normalize(migmres_mv *X, const migmres_mv *Q, double *C, int ldc,
+                                   double *B, int ldb, int *rank);
+int migmres_icgs_normalize(migmres_mv *X, double *B, int ldb, int *rank);
+
+/* ---------------- solver manager (Belos::BlockGmresSolMgr) ---------------- */
+
+int migmres_solver_create(migmres_ctx *ctx, migmres_solver **out);
+int migmres_solver_destroy(migmres_solver *s);
+/* Belos ParameterList names: "Block Size", "Num Blocks", "Maximum Iterations",
+ * "Maximum Restarts", "Convergence Tolerance", "Adaptive Block Size",
+ * "Orthogonalization" ("ICGS"), "Verbosity", "Output Frequency". */
+int migmres_solver_set_int(migmres_solver *s, const char *name, long long value);
+int migmres_solver_set_double(migmres_solver *s, const char *name, double value);
+int migmres_solver_set_string(migmres_solver *s, const char *name, const char *value);
+/* LinearProblem(A, X, B).setProblem() + solve(); X is updated in place.
+ * *converged = 1 for Belos::Converged, 0 for Unconverged. */
+int migmres_solver_solve(migmres_solver *s, migmres_crs *A, migmres_mv *X, const migmres_mv *B,
+                         int *converged);
+int migmres_solver_num_iters(const migmres_solver *s, int *iters);
+int migmres_solver_achieved_tol(const migmres_solver *s, double *tol);
+int migmres_solver_loa_detected(const migmres_solver *s, int *loa);
+/* Implicit residual history: one row of numrhs scaled norms per status-test check.
+ * Returns the number of rows via *nrows; pass out == NULL to query. */
+int migmres_solver_history(const migmres_solver *s, double *out, int *nrows, int *ncols);
+/* Counters: [0] operator applies, [1] explicit residual checks, [2] restarts,
+ * [3] blkOrthoSing fallbacks, [4] block iterations. */
+int migmres_solver_counters(const migmres_solver *s, long long *out, int n);
+/* Seconds spent in named phases: [0] total solve, [1] SpMM, [2] orthogonalization,
+ * [3] host least-squares, [4] communication. */
+int migmres_solver_timers(const migmres_solver *s, double *out, int n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MIGMRES_H */

@@ -1,0 +1,103 @@
+// Internal declarations shared by the migmres host runtime and the HIP kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/migmres.h"
+
+namespace migmres {
+
+// Error carried across the C ABI as (code, message).
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string &m) : std::runtime_error(m), code(c) {}
+};
+
+// Thread-local message behind migmres_last_error().
+void set_last_error(const std::string &msg);
+
+// Run f, translating exceptions into the C ABI's (code, message) convention.
+template <class F>
+int guard(F &&f) {
+  try {
+    f();
+    return MIGMRES_OK;
+  } catch (const Error &e) {
+    set_last_error(e.what());
+    return e.code;
+  } catch (const std::bad_alloc &) {
+    set_last_error("out of host memory");
+    return MIGMRES_ENOMEM;
+  } catch (const std::exception &e) {
+    set_last_error(e.what());
+    return MIGMRES_EINVAL;
+  }
+}
+
+#define MIG_HIP(call)                                                                      \
+  do {                                                                                     \
+    hipError_t e_ = (call);                                                                \
+    if (e_ != hipSuccess)                                                                  \
+      throw ::migmres::Error(MIGMRES_EHIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+#define MIG_CHECK(cond, msg)                                                               \
+  do {                                                                                     \
+    if (!(cond)) throw ::migmres::Error(MIGMRES_EINVAL, msg);                              \
+  } while (0)
+
+// Column-block descriptor handed to kernels by value.  Column c of the block starts at
+// base + (cols ? cols[c] : c) * ld; rows are contiguous (column-major, Epetra layout).
+struct MvDesc {
+  double *base;
+  long long ld;
+  const int *cols;  // device column table for non-contiguous views, else nullptr
+  int ncols;
+};
+
+// ---------------------------------------------------------------------------------
+// Kernel launchers (kernels.hip).  All are asynchronous on `s`.
+// ---------------------------------------------------------------------------------
+
+// Y[:,c] = alpha * (A X)[:,c] + beta * Y[:,c] for the local CSR rows.  Column ids
+// >= n_local index the ghost block (column-major, leading dim ldg).  Row sums are
+// accumulated in stored order without contraction (Epetra GeneralMM order).
+void launch_spmm(hipStream_t s, int row_begin, int row_end, const int *rowptr, const int *cols,
+                 const double *vals, MvDesc X, int n_local, const double *ghost, long long ldg,
+                 MvDesc Y, double alpha, double beta);
+
+// Partial products for C = A^T B over `nrows` rows: writes nblocks x (L*kb) partials.
+int gemm_tn_blocks(int nrows);
+void launch_gemm_tn_partial(hipStream_t s, MvDesc A, int L, MvDesc B, int kb, int nrows,
+                            double *partial, int nblocks);
+// out[o] = alpha * sum_b partial[b*nout + o] (fixed order: deterministic).
+void launch_reduce_partials(hipStream_t s, const double *partial, int nblocks, int nout,
+                            double alpha, double *out);
+
+// X = beta*X + alpha * A * M, M (L x kx) device column-major with leading dim ldm.
+void launch_gemm_nn(hipStream_t s, MvDesc A, int L, const double *M, int ldm, MvDesc X,
+                    int nrows, double alpha, double beta);
+
+// Per-column reductions: op 0 = sum a*b, 1 = sum |a|, 2 = max |a|.  Partials nblocks x k.
+int coldot_blocks(int nrows);
+void launch_coldot_partial(hipStream_t s, MvDesc A, MvDesc B, int nrows, int op, double *partial,
+                           int nblocks);
+void launch_reduce_max(hipStream_t s, const double *partial, int nblocks, int nout, double *out);
+
+// Elementwise: Y = alpha*A + beta*B ; Y *= alpha (or alphas[c]) ; Y = v ; Y = A.
+void launch_axpby(hipStream_t s, double alpha, MvDesc A, double beta, MvDesc B, MvDesc Y, int nrows);
+void launch_scale(hipStream_t s, MvDesc Y, int nrows, double alpha, const double *alphas);
+void launch_fill(hipStream_t s, MvDesc Y, int nrows, double v);
+void launch_copy(hipStream_t s, MvDesc A, MvDesc Y, int nrows);
+// Epetra_MultiVector::Random semantics over global rows [first, first+nrows).
+void launch_random(hipStream_t s, MvDesc Y, int nrows, long long first, long long n_global,
+                   unsigned int seed);
+// send[c*count + i] = X[lids[i], c]
+void launch_pack(hipStream_t s, MvDesc X, const int *lids, int count, double *send, int k);
+
+}  // namespace migmres

@@ -1,0 +1,188 @@
+// Host-side index maps: uniform row map, Epetra column map, import plan, local CRS and the
+// Galeri stencil generators.  Pure C++ (no GPU calls) so the plans are testable on a CPU.
+#include "plan.h"
+
+#include <algorithm>
+#include <cstring>
+#include <numeric>
+#include <unordered_map>
+#include <unordered_set>
+
+namespace migmres {
+
+// Epetra_BlockMap::ConstructAutoUniform (epetra/src/Epetra_BlockMap.cpp:60-107).
+void uniform_map(long long n_global, int nranks, int rank, long long *first, int *n_local) {
+  const long long base = n_global / nranks;
+  const long long rem = n_global % nranks;
+  long long start = (long long)rank * (base + 1);
+  long long n = base;
+  if (rank < rem)
+    n += 1;
+  else
+    start -= rank - rem;
+  *first = start;
+  *n_local = (int)n;
+}
+
+int owner_of(long long gid, long long n_global, int nranks) {
+  const long long base = n_global / nranks;
+  const long long rem = n_global % nranks;
+  const long long cut = rem * (base + 1);
+  if (gid < cut) return (int)(gid / (base + 1));
+  return (int)(rem + (gid - cut) / (base > 0 ? base : 1));
+}
+
+// Epetra_Util::Sort, ascending, int keys (epetra/src/Epetra_Util.cpp:113-156): the
+// gap-halving shell sort.  Not stable; companions move with their keys.
+void epetra_shell_sort(std::vector<int> &keys, std::vector<long long> *c1, std::vector<int> *c2) {
+  const int n = (int)keys.size();
+  int m = n / 2;
+  while (m > 0) {
+    const int max = n - m;
+    for (int j = 0; j < max; ++j) {
+      for (int k = j; k >= 0; k -= m) {
+        if (keys[k + m] >= keys[k]) break;
+        std::swap(keys[k + m], keys[k]);
+        if (c1) std::swap((*c1)[k + m], (*c1)[k]);
+        if (c2) std::swap((*c2)[k + m], (*c2)[k]);
+      }
+    }
+    m = m / 2;
+  }
+}
+
+// Epetra_CrsGraph::MakeColMap_int (epetra/src/Epetra_CrsGraph.cpp:1348-1524), default
+// SortGhostsAssociatedWithEachProcessor_ = false.
+std::vector<long long> make_colmap(long long n_global, int nranks, long long first, int n_local,
+                                   const long long *rowptr, const long long *gcols) {
+  std::vector<char> present((size_t)n_local, 0);
+  long long n_present = 0;
+  std::vector<long long> remote;
+  std::unordered_set<long long> seen;
+  const long long nnz = rowptr[n_local];
+  for (long long e = 0; e < nnz; ++e) {
+    const long long g = gcols[e];
+    if (g >= first && g < first + n_local) {
+      char &p = present[(size_t)(g - first)];
+      if (!p) {
+        p = 1;
+        ++n_present;
+      }
+    } else if (seen.insert(g).second) {
+      remote.push_back(g);
+    }
+  }
+  if (nranks == 1) {
+    if (!remote.empty()) throw Error(MIGMRES_EINVAL, "column ids outside the domain map on one rank");
+    if (n_present == n_local) {
+      std::vector<long long> cm((size_t)n_local);
+      std::iota(cm.begin(), cm.end(), first);
+      return cm;
+    }
+  }
+  std::vector<int> pids(remote.size());
+  for (size_t i = 0; i < remote.size(); ++i) pids[i] = owner_of(remote[i], n_global, nranks);
+  epetra_shell_sort(pids, &remote, nullptr);
+  std::vector<long long> cm;
+  cm.reserve((size_t)n_present + remote.size());
+  for (int i = 0; i < n_local; ++i)
+    if (present[(size_t)i] || n_present == n_local) cm.push_back(first + i);
+  cm.insert(cm.end(), remote.begin(), remote.end());
+  return cm;
+}
+
+// Remote part of Epetra_Import::Construct (epetra/src/Epetra_Import.cpp:292-440).
+RemotePlan make_remotes(long long n_global, int nranks, long long first, int n_local,
+                        const long long *colmap, int n_cols) {
+  RemotePlan p;
+  const int mn = std::min(n_local, n_cols);
+  int same = 0;
+  while (same < mn && colmap[same] == first + same) ++same;
+  p.num_same = same;
+  for (int i = same; i < n_cols; ++i) {
+    const long long g = colmap[i];
+    if (g >= first && g < first + n_local) {
+      p.permute_to.push_back(i);
+      p.permute_from.push_back((int)(g - first));
+    } else {
+      p.remote_lids.push_back(i);
+      p.remote_gids.push_back(g);
+      p.remote_pids.push_back(owner_of(g, n_global, nranks));
+    }
+  }
+  epetra_shell_sort(p.remote_pids, &p.remote_gids, &p.remote_lids);
+  return p;
+}
+
+// MakeIndicesLocal + SortEntries (epetra/src/Epetra_CrsMatrix.cpp:1147-1199): local ids via
+// the column map, each row's entries ordered by ascending local id.
+void local_crs(int n_local, const long long *rowptr, const long long *gcols, const double *vals,
+               const long long *colmap, int n_cols, long long first, int *lcols_out,
+               double *vals_out) {
+  // Owned GIDs map by offset when the column map starts with the whole domain.
+  int same = 0;
+  while (same < std::min(n_local, n_cols) && colmap[same] == first + same) ++same;
+  std::unordered_map<long long, int> lut;
+  for (int i = same; i < n_cols; ++i) lut.emplace(colmap[i], i);
+  std::vector<std::pair<int, double>> row;
+  for (int r = 0; r < n_local; ++r) {
+    const long long b = rowptr[r], e = rowptr[r + 1];
+    row.clear();
+    for (long long q = b; q < e; ++q) {
+      const long long g = gcols[q];
+      int lid;
+      if (g >= first && g < first + same)
+        lid = (int)(g - first);
+      else {
+        auto it = lut.find(g);
+        if (it == lut.end()) throw Error(MIGMRES_EINVAL, "column id missing from column map");
+        lid = it->second;
+      }
+      row.emplace_back(lid, vals[q]);
+    }
+    std::sort(row.begin(), row.end(),
+              [](const std::pair<int, double> &a, const std::pair<int, double> &b) { return a.first < b.first; });
+    for (size_t i = 0; i < row.size(); ++i) {
+      lcols_out[b + (long long)i] = row[i].first;
+      vals_out[b + (long long)i] = row[i].second;
+    }
+  }
+}
+
+// Galeri Cross2D / Cross3D rows in InsertGlobalValues order
+// (galeri/src-epetra/CrsMatrices/Galeri_Cross2D.h, Galeri_Cross3D.h:78-128;
+// neighbours: galeri/src-epetra/Galeri_Utils.cpp:331-398).
+void galeri_rows(const std::string &kind, int nx, int ny, int nz, long long first, int n_local,
+                 std::vector<long long> &rowptr, std::vector<long long> &gcols,
+                 std::vector<double> &vals) {
+  const bool three = kind == "Laplace3D";
+  if (!three && kind != "Laplace2D") throw Error(MIGMRES_EINVAL, "unknown Galeri matrix " + kind);
+  const long long nxy = (long long)nx * ny;
+  const int w = three ? 7 : 5;
+  rowptr.assign((size_t)n_local + 1, 0);
+  gcols.clear();
+  vals.clear();
+  gcols.reserve((size_t)n_local * w);
+  vals.reserve((size_t)n_local * w);
+  const double diag = three ? 6.0 : 4.0;
+  for (int r = 0; r < n_local; ++r) {
+    const long long g = first + r;
+    const long long ixy = three ? g % nxy : g;
+    const long long iz = three ? g / nxy : 0;
+    const long long ix = ixy % nx, iy = ixy / nx;
+    const long long zoff = iz * nxy;
+    if (ix != 0) { gcols.push_back(ixy - 1 + zoff); vals.push_back(-1.0); }
+    if (ix != nx - 1) { gcols.push_back(ixy + 1 + zoff); vals.push_back(-1.0); }
+    if (iy != 0) { gcols.push_back(ixy - nx + zoff); vals.push_back(-1.0); }
+    if (iy != ny - 1) { gcols.push_back(ixy + nx + zoff); vals.push_back(-1.0); }
+    if (three) {
+      if (iz != 0) { gcols.push_back(g - nxy); vals.push_back(-1.0); }
+      if (iz != nz - 1) { gcols.push_back(g + nxy); vals.push_back(-1.0); }
+    }
+    gcols.push_back(g);
+    vals.push_back(diag);
+    rowptr[(size_t)r + 1] = (long long)gcols.size();
+  }
+}
+
+}  // namespace migmres

@@ -1,0 +1,712 @@
+// Context, multivectors, distributed CRS operator and the C ABI for them.
+#include "runtime.h"
+
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <string>
+
+using namespace migmres;
+
+// ------------------------------------------------------------------------------------
+// error plumbing for the C ABI
+// ------------------------------------------------------------------------------------
+static thread_local std::string g_last_error;
+void migmres::set_last_error(const std::string &m) { g_last_error = m; }
+
+namespace {
+#define MIG_NCCL(call)                                                                      \
+  do {                                                                                      \
+    ncclResult_t r_ = (call);                                                               \
+    if (r_ != ncclSuccess) throw Error(MIGMRES_ERCCL, std::string(#call) + ": " + ncclGetErrorString(r_)); \
+  } while (0)
+
+long long round_up(long long a, long long b) { return (a + b - 1) / b * b; }
+}  // namespace
+
+extern "C" int migmres_abi_version(void) { return MIGMRES_ABI_VERSION; }
+extern "C" const char *migmres_last_error(void) { return g_last_error.c_str(); }
+
+// ------------------------------------------------------------------------------------
+// context
+// ------------------------------------------------------------------------------------
+static double *grow(double *&p, size_t &cap, size_t n) {
+  if (n <= cap) return p;
+  if (p) MIG_HIP(hipFree(p));
+  size_t c = n < 4096 ? 4096 : n;
+  MIG_HIP(hipMalloc(&p, c * sizeof(double)));
+  cap = c;
+  return p;
+}
+double *migmres_ctx::partial(size_t n) { return grow(d_partial, partial_cap, n); }
+double *migmres_ctx::red(size_t n) { return grow(d_red, red_cap, n); }
+double *migmres_ctx::coef(size_t n) { return grow(d_coef, coef_cap, n); }
+double *migmres_ctx::pinned(size_t n) {
+  if (n > pinned_cap) {
+    if (h_pinned) MIG_HIP(hipHostFree(h_pinned));
+    size_t c = n < 65536 ? 65536 : n;
+    MIG_HIP(hipHostMalloc(&h_pinned, c * sizeof(double), hipHostMallocDefault));
+    pinned_cap = c;
+  }
+  return h_pinned;
+}
+void migmres_ctx::allreduce(double *d, size_t n, bool max) {
+  if (nranks == 1 || n == 0) return;
+  auto t0 = std::chrono::steady_clock::now();
+  MIG_NCCL(ncclAllReduce(d, d, n, ncclDouble, max ? ncclMax : ncclSum, comm, stream));
+  MIG_HIP(hipStreamSynchronize(stream));
+  comm_seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
+extern "C" int migmres_comm_unique_id(unsigned char out[128]) {
+  return guard([&] {
+    ncclUniqueId id;
+    MIG_NCCL(ncclGetUniqueId(&id));
+    static_assert(sizeof(id) == 128, "RCCL unique id size");
+    std::memcpy(out, &id, 128);
+  });
+}
+
+extern "C" int migmres_ctx_create(int device, int rank, int nranks, const unsigned char *uid,
+                                  migmres_ctx **out) {
+  return guard([&] {
+    MIG_CHECK(out && nranks >= 1 && rank >= 0 && rank < nranks, "bad context arguments");
+    auto *c = new migmres_ctx();
+    c->device = device;
+    c->rank = rank;
+    c->nranks = nranks;
+    try {
+      MIG_HIP(hipSetDevice(device));
+      MIG_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+      if (nranks > 1) {
+        MIG_CHECK(uid != nullptr, "unique id required for nranks > 1");
+        ncclUniqueId id;
+        std::memcpy(&id, uid, 128);
+        MIG_NCCL(ncclCommInitRank(&c->comm, nranks, id, rank));
+      }
+    } catch (...) {
+      delete c;
+      throw;
+    }
+    *out = c;
+  });
+}
+
+extern "C" int migmres_ctx_destroy(migmres_ctx *c) {
+  return guard([&] {
+    if (!c) return;
+    hipStreamSynchronize(c->stream);
+    if (c->comm) ncclCommDestroy(c->comm);
+    if (c->d_partial) hipFree(c->d_partial);
+    if (c->d_red) hipFree(c->d_red);
+    if (c->d_coef) hipFree(c->d_coef);
+    if (c->h_pinned) hipHostFree(c->h_pinned);
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+  });
+}
+
+extern "C" int migmres_ctx_sync(migmres_ctx *c) {
+  return guard([&] { MIG_HIP(hipStreamSynchronize(c->stream)); });
+}
+
+extern "C" int migmres_ctx_rank(const migmres_ctx *c, int *rank, int *nranks) {
+  return guard([&] {
+    *rank = c->rank;
+    *nranks = c->nranks;
+  });
+}
+
+extern "C" int migmres_ctx_sum_all(migmres_ctx *c, const double *in, double *out, int n) {
+  return guard([&] {
+    if (n <= 0) return;
+    double *d = c->red((size_t)n);
+    MIG_HIP(hipMemcpyAsync(d, in, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+    c->allreduce(d, (size_t)n);
+    MIG_HIP(hipMemcpyAsync(out, d, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
+    MIG_HIP(hipStreamSynchronize(c->stream));
+  });
+}
+
+// ------------------------------------------------------------------------------------
+// multivectors
+// ------------------------------------------------------------------------------------
+migmres_mv::~migmres_mv() {
+  if (d_cols) hipFree(d_cols);
+  if (owner && base) hipFree(base);
+}
+
+namespace migmres {
+
+migmres_mv *mv_create(migmres_ctx *ctx, long long n_global, int n_local, int ncols) {
+  MIG_CHECK(ctx && n_local >= 0 && ncols >= 0, "bad multivector shape");
+  auto *m = new migmres_mv();
+  m->ctx = ctx;
+  m->n_global = n_global;
+  m->n_local = n_local;
+  m->ncols = ncols;
+  m->ld = round_up(n_local > 0 ? n_local : 1, 64);
+  m->owner = true;
+  const size_t bytes = (size_t)m->ld * (size_t)(ncols > 0 ? ncols : 1) * sizeof(double) + 256;
+  hipError_t e = hipMalloc(&m->base, bytes);
+  if (e != hipSuccess) {
+    delete m;
+    throw Error(MIGMRES_ENOMEM, std::string("hipMalloc multivector: ") + hipGetErrorString(e));
+  }
+  return m;
+}
+
+migmres_mv *mv_view(migmres_mv *p, const int *idx, int n) {
+  MIG_CHECK(p && n >= 0, "bad view");
+  bool contiguous = true;
+  for (int i = 0; i < n; ++i) {
+    MIG_CHECK(idx[i] >= 0 && idx[i] < p->ncols, "view index out of range");
+    if (i > 0 && idx[i] != idx[i - 1] + 1) contiguous = false;
+  }
+  auto *m = new migmres_mv();
+  m->ctx = p->ctx;
+  m->n_global = p->n_global;
+  m->n_local = p->n_local;
+  m->ncols = n;
+  m->ld = p->ld;
+  m->owner = false;
+  if (contiguous && p->contiguous()) {
+    m->base = p->base + (n > 0 ? (long long)idx[0] * p->ld : 0);
+    return m;
+  }
+  m->base = p->base;
+  m->cols.resize((size_t)n);
+  for (int i = 0; i < n; ++i) m->cols[(size_t)i] = p->contiguous() ? idx[i] : p->cols[(size_t)idx[i]];
+  if (n > 0) {
+    MIG_HIP(hipMalloc(&m->d_cols, sizeof(int) * n));
+    MIG_HIP(hipMemcpy(m->d_cols, m->cols.data(), sizeof(int) * n, hipMemcpyHostToDevice));
+  }
+  return m;
+}
+
+migmres_mv *mv_view_range(migmres_mv *p, int first, int n) {
+  std::vector<int> idx((size_t)n);
+  for (int i = 0; i < n; ++i) idx[(size_t)i] = first + i;
+  return mv_view(p, idx.data(), n);
+}
+
+static void same_rows(const migmres_mv &a, const migmres_mv &b) {
+  MIG_CHECK(a.n_local == b.n_local && a.n_global == b.n_global, "multivector row maps differ");
+}
+
+void mv_times_mat_add_mv(double alpha, const migmres_mv &A, const double *B, int ldb, double beta,
+                         migmres_mv &Y) {
+  same_rows(A, Y);
+  migmres_ctx *c = Y.ctx;
+  const int L = A.ncols, k = Y.ncols;
+  if (k == 0) return;
+  if (L == 0 || alpha == 0.0) {
+    if (beta == 0.0)
+      launch_fill(c->stream, Y.desc(), Y.n_local, 0.0);
+    else if (beta != 1.0)
+      launch_scale(c->stream, Y.desc(), Y.n_local, beta, nullptr);
+    return;
+  }
+  double *h = c->pinned((size_t)L * k);
+  for (int j = 0; j < k; ++j)
+    for (int i = 0; i < L; ++i) h[(size_t)i + (size_t)j * L] = B[(size_t)i + (size_t)j * ldb];
+  double *d = c->coef((size_t)L * k);
+  MIG_HIP(hipMemcpyAsync(d, h, sizeof(double) * L * k, hipMemcpyHostToDevice, c->stream));
+  launch_gemm_nn(c->stream, A.desc(), L, d, L, Y.desc(), Y.n_local, alpha, beta);
+  // the pinned staging buffer is reused by the next call: keep the copy ordered
+  MIG_HIP(hipStreamSynchronize(c->stream));
+}
+
+void mv_add_mv(double alpha, const migmres_mv &A, double beta, const migmres_mv &B, migmres_mv &Y) {
+  same_rows(A, Y);
+  same_rows(B, Y);
+  MIG_CHECK(A.ncols == Y.ncols && B.ncols == Y.ncols, "MvAddMv column counts differ");
+  launch_axpby(Y.ctx->stream, alpha, A.desc(), beta, B.desc(), Y.desc(), Y.n_local);
+}
+
+void mv_scale(migmres_mv &Y, double alpha) {
+  launch_scale(Y.ctx->stream, Y.desc(), Y.n_local, alpha, nullptr);
+}
+
+void mv_scale_vec(migmres_mv &Y, const double *alphas) {
+  migmres_ctx *c = Y.ctx;
+  double *d = c->coef((size_t)Y.ncols);
+  MIG_HIP(hipMemcpyAsync(d, alphas, sizeof(double) * Y.ncols, hipMemcpyHostToDevice, c->stream));
+  launch_scale(c->stream, Y.desc(), Y.n_local, 1.0, d);
+  MIG_HIP(hipStreamSynchronize(c->stream));
+}
+
+void mv_trans_mv(double alpha, const migmres_mv &A, const migmres_mv &B, double *C, int ldc) {
+  same_rows(A, B);
+  migmres_ctx *c = A.ctx;
+  const int L = A.ncols, kb = B.ncols;
+  if (L == 0 || kb == 0) return;
+  double *red = c->red((size_t)L * kb);
+  const int nblk = gemm_tn_blocks(A.n_local);
+  // Column chunks: A in 512-column slabs, B in 16-column slabs; views stay alive until the
+  // stream is drained because kernels read their column tables.
+  std::vector<migmres_mv *> views;
+  try {
+    for (int b0 = 0; b0 < kb; b0 += 16) {
+      const int kc = (kb - b0) < 16 ? (kb - b0) : 16;
+      migmres_mv *Bv = mv_view_range(const_cast<migmres_mv *>(&B), b0, kc);
+      views.push_back(Bv);
+      for (int a0 = 0; a0 < L; a0 += 512) {
+        const int lc = (L - a0) < 512 ? (L - a0) : 512;
+        migmres_mv *Av = mv_view_range(const_cast<migmres_mv *>(&A), a0, lc);
+        views.push_back(Av);
+        double *part = c->partial((size_t)nblk * lc * kc);
+        double *tmp = c->coef((size_t)lc * kc);
+        launch_gemm_tn_partial(c->stream, Av->desc(), lc, Bv->desc(), kc, A.n_local, part, nblk);
+        launch_reduce_partials(c->stream, part, nblk, lc * kc, alpha, tmp);
+        MIG_HIP(hipMemcpy2DAsync(red + a0 + (size_t)b0 * L, sizeof(double) * L, tmp,
+                                 sizeof(double) * lc, sizeof(double) * lc, kc,
+                                 hipMemcpyDeviceToDevice, c->stream));
+        if (L > 512 || kb > 16) MIG_HIP(hipStreamSynchronize(c->stream));  // scratch reuse
+      }
+    }
+  } catch (...) {
+    hipStreamSynchronize(c->stream);
+    for (auto *v : views) delete v;
+    throw;
+  }
+  c->allreduce(red, (size_t)L * kb);
+  double *h = c->pinned((size_t)L * kb);
+  MIG_HIP(hipMemcpyAsync(h, red, sizeof(double) * L * kb, hipMemcpyDeviceToHost, c->stream));
+  MIG_HIP(hipStreamSynchronize(c->stream));
+  for (auto *v : views) delete v;
+  for (int j = 0; j < kb; ++j)
+    for (int i = 0; i < L; ++i) C[(size_t)i + (size_t)j * ldc] = h[(size_t)i + (size_t)j * L];
+}
+
+static void coldot_reduce(const migmres_mv &A, const migmres_mv &B, int op, double *out) {
+  migmres_ctx *c = A.ctx;
+  const int k = A.ncols;
+  if (k == 0) return;
+  const int nblk = coldot_blocks(A.n_local);
+  double *part = c->partial((size_t)nblk * k);
+  double *red = c->red((size_t)k);
+  launch_coldot_partial(c->stream, A.desc(), B.desc(), A.n_local, op, part, nblk);
+  if (op == 2)
+    launch_reduce_max(c->stream, part, nblk, k, red);
+  else
+    launch_reduce_partials(c->stream, part, nblk, k, 1.0, red);
+  c->allreduce(red, (size_t)k, op == 2);
+  double *h = c->pinned((size_t)k);
+  MIG_HIP(hipMemcpyAsync(h, red, sizeof(double) * k, hipMemcpyDeviceToHost, c->stream));
+  MIG_HIP(hipStreamSynchronize(c->stream));
+  std::memcpy(out, h, sizeof(double) * k);
+}
+
+void mv_dot(const migmres_mv &A, const migmres_mv &B, double *out) {
+  same_rows(A, B);
+  MIG_CHECK(A.ncols == B.ncols, "MvDot column counts differ");
+  coldot_reduce(A, B, 0, out);
+}
+
+void mv_norm(const migmres_mv &A, double *out, int type) {
+  if (type == MIGMRES_TWO_NORM) {
+    coldot_reduce(A, A, 0, out);
+    for (int i = 0; i < A.ncols; ++i) out[i] = std::sqrt(out[i]);
+  } else if (type == MIGMRES_ONE_NORM) {
+    coldot_reduce(A, A, 1, out);
+  } else {
+    coldot_reduce(A, A, 2, out);
+  }
+}
+
+void mv_init(migmres_mv &Y, double alpha) { launch_fill(Y.ctx->stream, Y.desc(), Y.n_local, alpha); }
+
+void mv_random(migmres_mv &Y, unsigned int *seed) {
+  migmres_ctx *c = Y.ctx;
+  long long first = 0;
+  int nl = 0;
+  uniform_map(Y.n_global, c->nranks, c->rank, &first, &nl);
+  if (nl != Y.n_local) {
+    // non-uniform row map: exclusive scan of local lengths
+    std::vector<double> lens((size_t)c->nranks, 0.0);
+    lens[(size_t)c->rank] = (double)Y.n_local;
+    double *d = c->red((size_t)c->nranks);
+    MIG_HIP(hipMemcpyAsync(d, lens.data(), sizeof(double) * c->nranks, hipMemcpyHostToDevice, c->stream));
+    c->allreduce(d, (size_t)c->nranks);
+    MIG_HIP(hipMemcpyAsync(lens.data(), d, sizeof(double) * c->nranks, hipMemcpyDeviceToHost, c->stream));
+    MIG_HIP(hipStreamSynchronize(c->stream));
+    first = 0;
+    for (int r = 0; r < c->rank; ++r) first += (long long)lens[(size_t)r];
+  }
+  launch_random(c->stream, Y.desc(), Y.n_local, first, Y.n_global, *seed);
+  // advance the stream past all global entries, as Random() on P=1 would
+  unsigned long long s = *seed, a = 16807ULL, e = (unsigned long long)Y.n_global * Y.ncols, acc = 1;
+  const unsigned long long m = 2147483647ULL;
+  while (e) {
+    if (e & 1ULL) acc = acc * a % m;
+    a = a * a % m;
+    e >>= 1;
+  }
+  *seed = (unsigned int)(s * acc % m);
+}
+
+void mv_assign(const migmres_mv &A, migmres_mv &Y) {
+  same_rows(A, Y);
+  MIG_CHECK(A.ncols == Y.ncols, "Assign column counts differ");
+  launch_copy(Y.ctx->stream, A.desc(), Y.desc(), Y.n_local);
+}
+
+}  // namespace migmres
+
+// ------------------------------------------------------------------------------------
+// distributed CRS operator
+// ------------------------------------------------------------------------------------
+migmres_crs::~migmres_crs() {
+  for (void *p : {(void *)d_rowptr, (void *)d_cols, (void *)d_export, (void *)d_vals,
+                  (void *)d_send, (void *)d_ghost})
+    if (p) hipFree(p);
+}
+
+namespace migmres {
+
+migmres_crs *crs_create(migmres_ctx *ctx, long long n_global, long long first, int n_local,
+                        const long long *rowptr, const long long *gcols, const double *vals) {
+  MIG_CHECK(ctx && n_local >= 0 && rowptr, "bad CRS arguments");
+  const long long nnz = rowptr[n_local];
+  MIG_CHECK(nnz < (1LL << 31), "local nnz must fit int32 row offsets");
+  auto *A = new migmres_crs();
+  try {
+    A->ctx = ctx;
+    A->n_global = n_global;
+    A->first = first;
+    A->n_local = n_local;
+    A->nnz = nnz;
+    A->colmap = make_colmap(n_global, ctx->nranks, first, n_local, rowptr, gcols);
+    A->n_cols = (int)A->colmap.size();
+    A->plan = make_remotes(n_global, ctx->nranks, first, n_local, A->colmap.data(), A->n_cols);
+    const RemotePlan &p = A->plan;
+    const int n_remote = (int)p.remote_lids.size();
+
+    // Epetra local ids (sorted rows) -> X-space ids: owned columns index the local rows,
+    // remote columns index the ghost block in import (PID-sorted) order.
+    std::vector<int> lcols((size_t)nnz);
+    std::vector<double> lvals((size_t)nnz);
+    local_crs(n_local, rowptr, gcols, vals, A->colmap.data(), A->n_cols, first, lcols.data(),
+              lvals.data());
+    std::vector<int> xspace((size_t)A->n_cols, -1);
+    for (int i = 0; i < A->n_cols; ++i) {
+      const long long g = A->colmap[(size_t)i];
+      if (g >= first && g < first + n_local) xspace[(size_t)i] = (int)(g - first);
+    }
+    for (int i = 0; i < n_remote; ++i) xspace[(size_t)p.remote_lids[(size_t)i]] = n_local + i;
+    for (auto &v : lcols) v = xspace[(size_t)v];
+
+    // neighbour groups of the receive side (remote list is grouped by owner PID)
+    for (int i = 0; i < n_remote;) {
+      int j = i;
+      while (j < n_remote && p.remote_pids[(size_t)j] == p.remote_pids[(size_t)i]) ++j;
+      A->recv_nbrs.push_back({p.remote_pids[(size_t)i], i, j - i});
+      i = j;
+    }
+    // export lists: every rank tells each owner which GIDs it needs, in its own order
+    // (Epetra_MpiDistributor::CreateFromRecvs with Deterministic = true).
+    if (ctx->nranks > 1) {
+      const int P = ctx->nranks;
+      std::vector<double> cnt((size_t)P * P, 0.0);
+      for (auto &nb : A->recv_nbrs) cnt[(size_t)ctx->rank * P + nb.pid] = nb.count;
+      double *dc = ctx->red((size_t)P * P);
+      MIG_HIP(hipMemcpyAsync(dc, cnt.data(), sizeof(double) * P * P, hipMemcpyHostToDevice, ctx->stream));
+      ctx->allreduce(dc, (size_t)P * P);
+      MIG_HIP(hipMemcpyAsync(cnt.data(), dc, sizeof(double) * P * P, hipMemcpyDeviceToHost, ctx->stream));
+      MIG_HIP(hipStreamSynchronize(ctx->stream));
+      long long *d_req = nullptr, *d_give = nullptr;
+      long long total_give = 0;
+      std::vector<int> give_off((size_t)P, 0), give_cnt((size_t)P, 0);
+      for (int q = 0; q < P; ++q) {
+        give_cnt[(size_t)q] = (q == ctx->rank) ? 0 : (int)cnt[(size_t)q * P + ctx->rank];
+        give_off[(size_t)q] = (int)total_give;
+        total_give += give_cnt[(size_t)q];
+      }
+      MIG_HIP(hipMalloc(&d_req, sizeof(long long) * (n_remote > 0 ? n_remote : 1)));
+      MIG_HIP(hipMalloc(&d_give, sizeof(long long) * (total_give > 0 ? total_give : 1)));
+      if (n_remote)
+        MIG_HIP(hipMemcpy(d_req, p.remote_gids.data(), sizeof(long long) * n_remote, hipMemcpyHostToDevice));
+      MIG_NCCL(ncclGroupStart());
+      for (auto &nb : A->recv_nbrs)
+        MIG_NCCL(ncclSend(d_req + nb.offset, nb.count, ncclInt64, nb.pid, ctx->comm, ctx->stream));
+      for (int q = 0; q < P; ++q)
+        if (give_cnt[(size_t)q] > 0)
+          MIG_NCCL(ncclRecv(d_give + give_off[(size_t)q], give_cnt[(size_t)q], ncclInt64, q, ctx->comm, ctx->stream));
+      MIG_NCCL(ncclGroupEnd());
+      std::vector<long long> give((size_t)total_give);
+      if (total_give)
+        MIG_HIP(hipMemcpyAsync(give.data(), d_give, sizeof(long long) * total_give, hipMemcpyDeviceToHost, ctx->stream));
+      MIG_HIP(hipStreamSynchronize(ctx->stream));
+      hipFree(d_req);
+      hipFree(d_give);
+      for (int q = 0; q < P; ++q) {
+        if (give_cnt[(size_t)q] == 0) continue;
+        A->send_nbrs.push_back({q, (int)A->export_lids.size(), give_cnt[(size_t)q]});
+        for (int i = 0; i < give_cnt[(size_t)q]; ++i) {
+          const long long g = give[(size_t)give_off[(size_t)q] + i];
+          MIG_CHECK(g >= first && g < first + n_local, "requested GID not owned here");
+          A->export_lids.push_back((int)(g - first));
+          A->export_pids.push_back(q);
+        }
+      }
+    }
+    // device copies
+    std::vector<int> rp32((size_t)n_local + 1);
+    for (int r = 0; r <= n_local; ++r) rp32[(size_t)r] = (int)rowptr[r];
+    MIG_HIP(hipMalloc(&A->d_rowptr, sizeof(int) * (n_local + 1)));
+    MIG_HIP(hipMalloc(&A->d_cols, sizeof(int) * (nnz > 0 ? nnz : 1)));
+    MIG_HIP(hipMalloc(&A->d_vals, sizeof(double) * (nnz > 0 ? nnz : 1)));
+    MIG_HIP(hipMemcpy(A->d_rowptr, rp32.data(), sizeof(int) * (n_local + 1), hipMemcpyHostToDevice));
+    if (nnz) {
+      MIG_HIP(hipMemcpy(A->d_cols, lcols.data(), sizeof(int) * nnz, hipMemcpyHostToDevice));
+      MIG_HIP(hipMemcpy(A->d_vals, lvals.data(), sizeof(double) * nnz, hipMemcpyHostToDevice));
+    }
+    if (!A->export_lids.empty()) {
+      MIG_HIP(hipMalloc(&A->d_export, sizeof(int) * A->export_lids.size()));
+      MIG_HIP(hipMemcpy(A->d_export, A->export_lids.data(), sizeof(int) * A->export_lids.size(),
+                        hipMemcpyHostToDevice));
+    }
+  } catch (...) {
+    delete A;
+    throw;
+  }
+  return A;
+}
+
+void crs_apply(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, double alpha, double beta) {
+  MIG_CHECK(X.n_local == A.n_local && Y.n_local == A.n_local, "apply: row maps differ");
+  MIG_CHECK(X.ncols == Y.ncols, "apply: column counts differ");
+  migmres_ctx *c = A.ctx;
+  const int k = X.ncols;
+  const int n_remote = (int)A.plan.remote_lids.size();
+  const int n_export = (int)A.export_lids.size();
+  if (c->nranks > 1 && (n_remote > 0 || n_export > 0)) {
+    if (k > A.halo_k) {
+      if (A.d_send) hipFree(A.d_send);
+      if (A.d_ghost) hipFree(A.d_ghost);
+      A.d_send = A.d_ghost = nullptr;
+      MIG_HIP(hipMalloc(&A.d_send, sizeof(double) * ((size_t)n_export * k + 1)));
+      MIG_HIP(hipMalloc(&A.d_ghost, sizeof(double) * ((size_t)n_remote * k + 1)));
+      A.halo_k = k;
+    }
+    auto t0 = std::chrono::steady_clock::now();
+    launch_pack(c->stream, X.desc(), A.d_export, n_export, A.d_send, k);
+    MIG_NCCL(ncclGroupStart());
+    for (auto &nb : A.send_nbrs)
+      for (int col = 0; col < k; ++col)
+        MIG_NCCL(ncclSend(A.d_send + (size_t)col * n_export + nb.offset, nb.count, ncclDouble, nb.pid,
+                          c->comm, c->stream));
+    for (auto &nb : A.recv_nbrs)
+      for (int col = 0; col < k; ++col)
+        MIG_NCCL(ncclRecv(A.d_ghost + (size_t)col * n_remote + nb.offset, nb.count, ncclDouble, nb.pid,
+                          c->comm, c->stream));
+    MIG_NCCL(ncclGroupEnd());
+    c->comm_seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
+  launch_spmm(c->stream, 0, A.n_local, A.d_rowptr, A.d_cols, A.d_vals, X.desc(), A.n_local,
+              A.d_ghost, n_remote, Y.desc(), alpha, beta);
+}
+
+}  // namespace migmres
+
+// ------------------------------------------------------------------------------------
+// C ABI: maps, plans, CRS, multivectors
+// ------------------------------------------------------------------------------------
+extern "C" int migmres_map_uniform(long long n_global, int nranks, int rank, long long *first,
+                                   int *n_local) {
+  return guard([&] {
+    MIG_CHECK(nranks >= 1 && rank >= 0 && rank < nranks && n_global >= 0, "bad map arguments");
+    uniform_map(n_global, nranks, rank, first, n_local);
+  });
+}
+
+extern "C" int migmres_plan_colmap(long long n_global, int nranks, long long first, int n_local,
+                                   const long long *rowptr, const long long *gcols,
+                                   long long *colmap_out, int *n_cols) {
+  return guard([&] {
+    auto cm = make_colmap(n_global, nranks, first, n_local, rowptr, gcols);
+    *n_cols = (int)cm.size();
+    if (colmap_out) std::memcpy(colmap_out, cm.data(), sizeof(long long) * cm.size());
+  });
+}
+
+extern "C" int migmres_plan_remotes(long long n_global, int nranks, long long first, int n_local,
+                                    const long long *colmap, int n_cols, int *num_same,
+                                    int *remote_lids, long long *remote_gids, int *remote_pids,
+                                    int *n_remote) {
+  return guard([&] {
+    RemotePlan p = make_remotes(n_global, nranks, first, n_local, colmap, n_cols);
+    *num_same = p.num_same;
+    *n_remote = (int)p.remote_lids.size();
+    for (size_t i = 0; i < p.remote_lids.size(); ++i) {
+      if (remote_lids) remote_lids[i] = p.remote_lids[i];
+      if (remote_gids) remote_gids[i] = p.remote_gids[i];
+      if (remote_pids) remote_pids[i] = p.remote_pids[i];
+    }
+  });
+}
+
+extern "C" int migmres_plan_local_crs(long long first, int n_local, const long long *rowptr,
+                                      const long long *gcols, const double *vals,
+                                      const long long *colmap, int n_cols, int *lcols_out,
+                                      double *vals_out) {
+  return guard([&] {
+    local_crs(n_local, rowptr, gcols, vals, colmap, n_cols, first, lcols_out, vals_out);
+  });
+}
+
+extern "C" int migmres_crs_create(migmres_ctx *ctx, long long n_global, long long first, int n_local,
+                                  const long long *rowptr, const long long *gcols, const double *vals,
+                                  migmres_crs **out) {
+  return guard([&] { *out = crs_create(ctx, n_global, first, n_local, rowptr, gcols, vals); });
+}
+
+extern "C" int migmres_crs_create_galeri(migmres_ctx *ctx, const char *kind, int nx, int ny, int nz,
+                                         migmres_crs **out) {
+  return guard([&] {
+    const std::string k(kind ? kind : "");
+    const long long n_global = (long long)nx * ny * (k == "Laplace3D" ? nz : 1);
+    long long first = 0;
+    int n_local = 0;
+    uniform_map(n_global, ctx->nranks, ctx->rank, &first, &n_local);
+    std::vector<long long> rp, gc;
+    std::vector<double> v;
+    galeri_rows(k, nx, ny, nz, first, n_local, rp, gc, v);
+    *out = crs_create(ctx, n_global, first, n_local, rp.data(), gc.data(), v.data());
+  });
+}
+
+extern "C" int migmres_crs_destroy(migmres_crs *A) {
+  return guard([&] { delete A; });
+}
+
+extern "C" int migmres_crs_info(const migmres_crs *A, long long *n_global, long long *first,
+                                int *n_local, int *n_cols, long long *nnz_local, int *n_remote,
+                                int *n_export) {
+  return guard([&] {
+    if (n_global) *n_global = A->n_global;
+    if (first) *first = A->first;
+    if (n_local) *n_local = A->n_local;
+    if (n_cols) *n_cols = A->n_cols;
+    if (nnz_local) *nnz_local = A->nnz;
+    if (n_remote) *n_remote = (int)A->plan.remote_lids.size();
+    if (n_export) *n_export = (int)A->export_lids.size();
+  });
+}
+
+extern "C" int migmres_crs_colmap(const migmres_crs *A, long long *out) {
+  return guard([&] { std::memcpy(out, A->colmap.data(), sizeof(long long) * A->colmap.size()); });
+}
+
+extern "C" int migmres_crs_import_plan(const migmres_crs *A, int *export_lids, int *export_pids,
+                                       int *remote_lids, int *remote_pids) {
+  return guard([&] {
+    for (size_t i = 0; i < A->export_lids.size(); ++i) {
+      if (export_lids) export_lids[i] = A->export_lids[i];
+      if (export_pids) export_pids[i] = A->export_pids[i];
+    }
+    for (size_t i = 0; i < A->plan.remote_lids.size(); ++i) {
+      if (remote_lids) remote_lids[i] = A->plan.remote_lids[i];
+      if (remote_pids) remote_pids[i] = A->plan.remote_pids[i];
+    }
+  });
+}
+
+extern "C" int migmres_crs_apply(migmres_crs *A, const migmres_mv *X, migmres_mv *Y, double alpha,
+                                 double beta) {
+  return guard([&] { crs_apply(*A, *X, *Y, alpha, beta); });
+}
+
+extern "C" int migmres_mv_create(migmres_ctx *ctx, long long n_global, int n_local, int ncols,
+                                 migmres_mv **out) {
+  return guard([&] { *out = mv_create(ctx, n_global, n_local, ncols); });
+}
+extern "C" int migmres_mv_view(migmres_mv *parent, const int *idx, int n, migmres_mv **out) {
+  return guard([&] { *out = mv_view(parent, idx, n); });
+}
+extern "C" int migmres_mv_view_range(migmres_mv *parent, int first, int n, migmres_mv **out) {
+  return guard([&] {
+    MIG_CHECK(first >= 0 && n >= 0 && first + n <= parent->ncols, "range out of bounds");
+    *out = mv_view_range(parent, first, n);
+  });
+}
+extern "C" int migmres_mv_destroy(migmres_mv *mv) {
+  return guard([&] { delete mv; });
+}
+extern "C" int migmres_mv_shape(const migmres_mv *mv, long long *n_global, int *n_local, int *ncols,
+                                int *constant_stride) {
+  return guard([&] {
+    if (n_global) *n_global = mv->n_global;
+    if (n_local) *n_local = mv->n_local;
+    if (ncols) *ncols = mv->ncols;
+    if (constant_stride) *constant_stride = mv->contiguous() ? 1 : 0;
+  });
+}
+extern "C" int migmres_mv_upload(migmres_mv *mv, const double *host, long long ld) {
+  return guard([&] {
+    MIG_CHECK(ld >= mv->n_local, "host leading dimension too small");
+    hipStream_t s = mv->ctx->stream;
+    for (int c = 0; c < mv->ncols; ++c)
+      MIG_HIP(hipMemcpyAsync(mv->base + mv->col_offset(c), host + (size_t)c * ld,
+                             sizeof(double) * mv->n_local, hipMemcpyHostToDevice, s));
+    MIG_HIP(hipStreamSynchronize(s));
+  });
+}
+extern "C" int migmres_mv_download(const migmres_mv *mv, double *host, long long ld) {
+  return guard([&] {
+    MIG_CHECK(ld >= mv->n_local, "host leading dimension too small");
+    hipStream_t s = mv->ctx->stream;
+    for (int c = 0; c < mv->ncols; ++c)
+      MIG_HIP(hipMemcpyAsync(host + (size_t)c * ld, mv->base + mv->col_offset(c),
+                             sizeof(double) * mv->n_local, hipMemcpyDeviceToHost, s));
+    MIG_HIP(hipStreamSynchronize(s));
+  });
+}
+extern "C" int migmres_mv_times_mat_add_mv(double alpha, const migmres_mv *A, const double *B, int ldb,
+                                           double beta, migmres_mv *mv) {
+  return guard([&] { mv_times_mat_add_mv(alpha, *A, B, ldb, beta, *mv); });
+}
+extern "C" int migmres_mv_add_mv(double alpha, const migmres_mv *A, double beta, const migmres_mv *B,
+                                 migmres_mv *mv) {
+  return guard([&] { mv_add_mv(alpha, *A, beta, *B, *mv); });
+}
+extern "C" int migmres_mv_scale(migmres_mv *mv, double alpha) {
+  return guard([&] { mv_scale(*mv, alpha); });
+}
+extern "C" int migmres_mv_scale_vec(migmres_mv *mv, const double *alphas) {
+  return guard([&] { mv_scale_vec(*mv, alphas); });
+}
+extern "C" int migmres_mv_trans_mv(double alpha, const migmres_mv *A, const migmres_mv *B, double *C,
+                                   int ldc) {
+  return guard([&] { mv_trans_mv(alpha, *A, *B, C, ldc); });
+}
+extern "C" int migmres_mv_dot(const migmres_mv *A, const migmres_mv *B, double *out) {
+  return guard([&] { mv_dot(*A, *B, out); });
+}
+extern "C" int migmres_mv_norm(const migmres_mv *mv, double *out, int norm_type) {
+  return guard([&] { mv_norm(*mv, out, norm_type); });
+}
+extern "C" int migmres_mv_init(migmres_mv *mv, double alpha) {
+  return guard([&] { mv_init(*mv, alpha); });
+}
+extern "C" int migmres_mv_random(migmres_mv *mv, unsigned int *seed) {
+  return guard([&] { mv_random(*mv, seed); });
+}
+extern "C" int migmres_mv_assign(const migmres_mv *A, migmres_mv *mv) {
+  return guard([&] { mv_assign(*A, *mv); });
+}
+extern "C" int migmres_mv_set_block(const migmres_mv *A, const int *idx, int n, migmres_mv *mv) {
+  return guard([&] {
+    MIG_CHECK(n == A->ncols, "SetBlock: index count must equal A's columns");
+    migmres_mv *v = mv_view(mv, idx, n);
+    try {
+      mv_assign(*A, *v);
+      MIG_HIP(hipStreamSynchronize(mv->ctx->stream));
+    } catch (...) {
+      delete v;
+      throw;
+    }
+    delete v;
+  });
+}

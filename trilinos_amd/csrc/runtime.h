@@ -1,0 +1,95 @@
+// Host runtime objects behind the C ABI: context (device, stream, RCCL communicator,
+// scratch), multivectors, the distributed CRS operator and the MultiVecTraits operations.
+#pragma once
+
+#include <rccl/rccl.h>
+
+#include <string>
+#include <vector>
+
+#include "internal.h"
+#include "plan.h"
+
+struct migmres_ctx {
+  int device = 0, rank = 0, nranks = 1;
+  hipStream_t stream = nullptr;
+  ncclComm_t comm = nullptr;
+  // device scratch: per-workgroup partials, reduced results, staged coefficients
+  double *d_partial = nullptr;
+  size_t partial_cap = 0;
+  double *d_red = nullptr;
+  size_t red_cap = 0;
+  double *d_coef = nullptr;
+  size_t coef_cap = 0;
+  double *h_pinned = nullptr;
+  size_t pinned_cap = 0;
+  double comm_seconds = 0.0;
+
+  double *partial(size_t n);
+  double *red(size_t n);
+  double *coef(size_t n);
+  double *pinned(size_t n);
+  // In-place sum (or max) all-reduce of n device doubles on the context stream.
+  void allreduce(double *d, size_t n, bool max = false);
+};
+
+struct migmres_mv {
+  migmres_ctx *ctx = nullptr;
+  long long n_global = 0;
+  int n_local = 0;
+  int ncols = 0;
+  long long ld = 0;
+  double *base = nullptr;
+  bool owner = false;
+  std::vector<int> cols;  // column offsets relative to base (empty: contiguous)
+  int *d_cols = nullptr;
+
+  migmres::MvDesc desc() const { return migmres::MvDesc{base, ld, d_cols, ncols}; }
+  bool contiguous() const { return cols.empty(); }
+  long long col_offset(int c) const { return (long long)(cols.empty() ? c : cols[(size_t)c]) * ld; }
+  ~migmres_mv();
+};
+
+struct migmres_crs {
+  migmres_ctx *ctx = nullptr;
+  long long n_global = 0, first = 0, nnz = 0;
+  int n_local = 0, n_cols = 0;
+  std::vector<long long> colmap;
+  migmres::RemotePlan plan;
+  std::vector<int> export_lids, export_pids;
+  struct Nbr {
+    int pid, offset, count;
+  };
+  std::vector<Nbr> recv_nbrs, send_nbrs;
+  int *d_rowptr = nullptr, *d_cols = nullptr, *d_export = nullptr;
+  double *d_vals = nullptr;
+  double *d_send = nullptr, *d_ghost = nullptr;
+  int halo_k = 0;
+  ~migmres_crs();
+};
+
+namespace migmres {
+
+migmres_mv *mv_create(migmres_ctx *ctx, long long n_global, int n_local, int ncols);
+migmres_mv *mv_view(migmres_mv *parent, const int *idx, int n);
+migmres_mv *mv_view_range(migmres_mv *parent, int first, int n);
+
+// Belos::MultiVecTraits operations (device data, host coefficient matrices).
+void mv_times_mat_add_mv(double alpha, const migmres_mv &A, const double *B, int ldb, double beta,
+                         migmres_mv &Y);
+void mv_add_mv(double alpha, const migmres_mv &A, double beta, const migmres_mv &B, migmres_mv &Y);
+void mv_scale(migmres_mv &Y, double alpha);
+void mv_scale_vec(migmres_mv &Y, const double *alphas);
+void mv_trans_mv(double alpha, const migmres_mv &A, const migmres_mv &B, double *C, int ldc);
+void mv_dot(const migmres_mv &A, const migmres_mv &B, double *out);
+void mv_norm(const migmres_mv &A, double *out, int type);
+void mv_init(migmres_mv &Y, double alpha);
+void mv_random(migmres_mv &Y, unsigned int *seed);
+void mv_assign(const migmres_mv &A, migmres_mv &Y);
+
+migmres_crs *crs_create(migmres_ctx *ctx, long long n_global, long long first, int n_local,
+                        const long long *rowptr, const long long *gcols, const double *vals);
+// Y = alpha*A*X + beta*Y including the halo import.
+void crs_apply(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, double alpha, double beta);
+
+}  // namespace migmres

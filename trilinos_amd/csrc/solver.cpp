@@ -1,0 +1,862 @@
+// Block GMRES solver manager, block Arnoldi iteration and ICGS orthogonalisation on
+// device multivectors.  Host C++ keeps exactly the reference's control flow and small
+// dense algebra; every N-sized operation is a HIP kernel (runtime.cpp / kernels.hip).
+//
+//   ICGS                 belos/src/BelosICGSOrthoManager.hpp:646-1701
+//   BlockGmresIter       belos/src/BelosBlockGmresIter.hpp:405-868
+//   StatusTestImpResNorm belos/src/BelosStatusTestImpResNorm.hpp:492-749, 808-845
+//   StatusTestMaxIters   belos/src/BelosStatusTestMaxIters.hpp:165-172
+//   LinearProblem        belos/src/BelosLinearProblem.hpp:642-1231
+//   BlockGmresSolMgr     belos/src/BelosBlockGmresSolMgr.hpp:430-1303
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <map>
+#include <memory>
+#include <string>
+
+#include "runtime.h"
+
+using namespace migmres;
+
+namespace {
+
+
+struct MvPtr {
+  migmres_mv *p = nullptr;
+  MvPtr() = default;
+  explicit MvPtr(migmres_mv *q) : p(q) {}
+  MvPtr(const MvPtr &) = delete;
+  MvPtr &operator=(const MvPtr &) = delete;
+  MvPtr(MvPtr &&o) noexcept : p(o.p) { o.p = nullptr; }
+  MvPtr &operator=(MvPtr &&o) noexcept {
+    reset();
+    p = o.p;
+    o.p = nullptr;
+    return *this;
+  }
+  ~MvPtr() { reset(); }
+  void reset() {
+    if (p) {
+      if (p->d_cols) hipStreamSynchronize(p->ctx->stream);
+      delete p;
+    }
+    p = nullptr;
+  }
+  migmres_mv &operator*() const { return *p; }
+  migmres_mv *operator->() const { return p; }
+};
+
+MvPtr view(migmres_mv &m, int first, int n) { return MvPtr(mv_view_range(&m, first, n)); }
+
+double dot1(const migmres_mv &a, const migmres_mv &b) {
+  double r = 0.0;
+  mv_dot(a, b, &r);
+  return r;
+}
+
+const double kEps = std::numeric_limits<double>::epsilon();
+
+// ------------------------------------------------------------------------------------
+// ICGS orthogonalisation manager (max_ortho_steps = 2, blk_tol = 10 sqrt(eps),
+// sing_tol = 10 eps: BelosICGSOrthoManager.hpp:561-573)
+// ------------------------------------------------------------------------------------
+struct Icgs {
+  int steps = 2;
+  double blk_tol = 10.0 * std::sqrt(kEps);
+  double sing_tol = 10.0 * kEps;
+  unsigned int seed = 12345u;  // MvRandom stream for rank-deficiency fallbacks
+  long long sing_count = 0;
+
+  // projectAndNormalizeWithMxImpl (BelosICGSOrthoManager.hpp:646-821).
+  // C is (Q.ncols x X.ncols, ldc), B is (X.ncols x X.ncols, ldb), both host.
+  int project_and_normalize(migmres_mv &X, migmres_mv &Q, double *C, int ldc, double *B, int ldb) {
+    const int xc = X.ncols;
+    if (xc == 1) {
+      blk_ortho1(X, Q, C, ldc);
+      const double d = dot1(X, X);
+      B[0] = std::sqrt(std::fabs(d));
+      if (std::fabs(B[0]) > 0.0) mv_scale(X, 1.0 / B[0]);
+      return 1;
+    }
+    MvPtr tmpX(mv_create(X.ctx, X.n_global, X.n_local, xc));
+    mv_assign(X, *tmpX);
+    int rank;
+    if (blk_ortho(X, Q, C, ldc)) {
+      rank = blk_ortho_sing(*tmpX, Q, C, ldc, B, ldb);
+      mv_assign(*tmpX, X);
+    } else {
+      rank = find_basis(X, B, ldb, false);
+      if (rank < xc) {
+        rank = blk_ortho_sing(*tmpX, Q, C, ldc, B, ldb);
+        mv_assign(*tmpX, X);
+      }
+    }
+    MIG_HIP(hipStreamSynchronize(X.ctx->stream));
+    return rank;
+  }
+
+  int normalize(migmres_mv &X, double *B, int ldb) { return find_basis(X, B, ldb, true); }
+
+  // blkOrtho1 (BelosICGSOrthoManager.hpp:1231-1322)
+  void blk_ortho1(migmres_mv &X, migmres_mv &Q, double *C, int ldc) {
+    const int L = Q.ncols, k = X.ncols;
+    mv_trans_mv(1.0, Q, X, C, ldc);
+    mv_times_mat_add_mv(-1.0, Q, C, ldc, 1.0, X);
+    std::vector<double> C2((size_t)L * k);
+    for (int s = 1; s < steps; ++s) {
+      mv_trans_mv(1.0, Q, X, C2.data(), L);
+      for (int j = 0; j < k; ++j)
+        for (int i = 0; i < L; ++i) C[i + (size_t)j * ldc] += C2[i + (size_t)j * L];
+      mv_times_mat_add_mv(-1.0, Q, C2.data(), L, 1.0, X);
+    }
+  }
+
+  // blkOrtho (BelosICGSOrthoManager.hpp:1328-1445); returns the dependency flag.
+  bool blk_ortho(migmres_mv &X, migmres_mv &Q, double *C, int ldc) {
+    const int L = Q.ncols, k = X.ncols;
+    std::vector<double> old_dot((size_t)k), new_dot((size_t)k);
+    mv_dot(X, X, old_dot.data());
+    blk_ortho1(X, Q, C, ldc);
+    mv_dot(X, X, new_dot.data());
+    (void)L;
+    for (int i = 0; i < k; ++i)
+      if (std::fabs(new_dot[(size_t)i]) < std::fabs(old_dot[(size_t)i] * blk_tol)) return true;
+    return false;
+  }
+
+  // findBasis (BelosICGSOrthoManager.hpp:936-1225), howMany = all columns.
+  int find_basis(migmres_mv &X, double *B, int ldb, bool complete) {
+    const int xc = X.ncols;
+    MvPtr old_xj(mv_create(X.ctx, X.n_global, X.n_local, 1));
+    std::vector<double> P2, product;
+    for (int j = 0; j < xc; ++j) {
+      MvPtr Xj = view(X, j, 1);
+      MvPtr prevX = view(X, 0, j);
+      bool add_vec = false;
+      if (j > 0) mv_assign(*Xj, *old_xj);
+      double old_dot = dot1(*Xj, *Xj);
+      if (old_dot < 0.0) throw Error(MIGMRES_ESTATE, "ICGS: negative definiteness in inner product");
+      product.assign((size_t)j, 0.0);
+      double new_dot;
+      if (j > 0) {
+        P2.assign((size_t)j, 0.0);
+        for (int s = 0; s < steps; ++s) {
+          mv_trans_mv(1.0, *prevX, *Xj, P2.data(), j);
+          mv_times_mat_add_mv(-1.0, *prevX, P2.data(), j, 1.0, *Xj);
+          for (int i = 0; i < j; ++i) product[(size_t)i] = (s == 0) ? P2[(size_t)i] : product[(size_t)i] + P2[(size_t)i];
+        }
+        new_dot = dot1(*Xj, *old_xj);
+      } else {
+        new_dot = old_dot;
+      }
+      if (complete) {
+        if (std::fabs(new_dot) < std::fabs(sing_tol * old_dot)) {
+          add_vec = true;
+          MvPtr t(mv_create(X.ctx, X.n_global, X.n_local, 1));
+          mv_random(*t, &seed);
+          old_dot = dot1(*t, *t);
+          std::vector<double> pr((size_t)(j > 0 ? j : 1));
+          for (int s = 0; s < steps && j > 0; ++s) {
+            mv_trans_mv(1.0, *prevX, *t, pr.data(), j);
+            mv_times_mat_add_mv(-1.0, *prevX, pr.data(), j, 1.0, *t);
+          }
+          new_dot = dot1(*t, *t);
+          if (std::fabs(new_dot) >= std::fabs(old_dot * sing_tol))
+            mv_assign(*t, *Xj);
+          else
+            return j;
+        }
+      } else if (std::fabs(new_dot) < std::fabs(old_dot * blk_tol)) {
+        return j;
+      }
+      const double diag = std::sqrt(std::fabs(new_dot));
+      mv_scale(*Xj, 1.0 / diag);
+      B[j + (size_t)j * ldb] = add_vec ? 0.0 : diag;
+      if (!add_vec)
+        for (int i = 0; i < j; ++i) B[i + (size_t)j * ldb] = product[(size_t)i];
+    }
+    return xc;
+  }
+
+  // blkOrthoSing (BelosICGSOrthoManager.hpp:1449-1701), including the reference's use of a
+  // newDot that is only refreshed on the random-vector path.
+  int blk_ortho_sing(migmres_mv &X, migmres_mv &Q, double *C, int ldc, double *B, int ldb) {
+    ++sing_count;
+    const int xc = X.ncols, L = Q.ncols;
+    double new_dot = 0.0;
+    std::vector<double> tc((size_t)L + xc), c2((size_t)L + xc);
+    for (int j = 0; j < xc; ++j) {
+      MvPtr Xj = view(X, j, 1);
+      MvPtr lastQ = view(X, 0, j);
+      migmres_mv *Qs[2] = {&Q, lastQ.p};
+      double *Cs[2] = {C, B};
+      const int lds[2] = {ldc, ldb};
+      const int nq = j > 0 ? 2 : 1;
+      double old_dot = dot1(*Xj, *Xj);
+      for (int i = 0; i < nq; ++i) {
+        const int q = Qs[i]->ncols;
+        double *col = Cs[i] + (size_t)j * lds[i];
+        mv_trans_mv(1.0, *Qs[i], *Xj, col, q);
+        mv_times_mat_add_mv(-1.0, *Qs[i], col, q, 1.0, *Xj);
+      }
+      for (int s = 1; s < steps; ++s) {
+        for (int i = 0; i < nq; ++i) {
+          const int q = Qs[i]->ncols;
+          double *col = Cs[i] + (size_t)j * lds[i];
+          mv_trans_mv(1.0, *Qs[i], *Xj, c2.data(), q);
+          for (int r = 0; r < q; ++r) col[r] += c2[(size_t)r];
+          mv_times_mat_add_mv(-1.0, *Qs[i], c2.data(), q, 1.0, *Xj);
+        }
+      }
+      const bool dep = std::fabs(new_dot) < std::fabs(old_dot * sing_tol);
+      if (!dep) {
+        const double diag = std::sqrt(std::fabs(new_dot));
+        mv_scale(*Xj, 1.0 / diag);
+        B[j + (size_t)j * ldb] = diag;
+      } else {
+        MvPtr t(mv_create(X.ctx, X.n_global, X.n_local, 1));
+        mv_random(*t, &seed);
+        old_dot = dot1(*t, *t);
+        for (int s = 0; s < steps; ++s)
+          for (int i = 0; i < nq; ++i) {
+            const int q = Qs[i]->ncols;
+            mv_trans_mv(1.0, *Qs[i], *t, tc.data(), q);
+            mv_times_mat_add_mv(-1.0, *Qs[i], tc.data(), q, 1.0, *t);
+          }
+        new_dot = dot1(*t, *t);
+        if (std::fabs(new_dot) >= std::fabs(old_dot * sing_tol)) {
+          const double diag = std::sqrt(std::fabs(new_dot));
+          B[j + (size_t)j * ldb] = 0.0;
+          mv_add_mv(1.0 / diag, *t, 0.0, *t, *Xj);
+        } else {
+          return j;
+        }
+      }
+    }
+    return xc;
+  }
+};
+
+// ------------------------------------------------------------------------------------
+// Small dense helpers (Teuchos::BLAS semantics, column-major)
+// ------------------------------------------------------------------------------------
+void rotg(double &a, double &b, double &c, double &s) {
+  const double roe = std::fabs(a) > std::fabs(b) ? a : b;
+  const double scale = std::fabs(a) + std::fabs(b);
+  if (scale == 0.0) {
+    c = 1.0;
+    s = 0.0;
+    a = 0.0;
+    b = 0.0;
+    return;
+  }
+  double r = scale * std::sqrt((a / scale) * (a / scale) + (b / scale) * (b / scale));
+  r = std::copysign(1.0, roe) * r;
+  c = a / r;
+  s = b / r;
+  double z = 1.0;
+  if (std::fabs(a) > std::fabs(b)) z = s;
+  if (std::fabs(b) >= std::fabs(a) && c != 0.0) z = 1.0 / c;
+  a = r;
+  b = z;
+}
+
+struct Params {
+  double tol = 1e-8;
+  int max_restarts = 20;
+  int max_iters = 1000;
+  int num_blocks = 300;
+  int block_size = 1;
+  bool adaptive = true;
+  std::string ortho = "DGKS";
+  int verbosity = 0;
+  int output_freq = -1;
+};
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------
+// Solver state
+// ------------------------------------------------------------------------------------
+struct migmres_solver {
+  migmres_ctx *ctx = nullptr;
+  Params p;
+  Icgs ortho;
+  // results
+  int num_iters = 0;
+  double achieved_tol = 0.0;
+  bool loa = false;
+  std::vector<double> history;
+  int hist_cols = 0;
+  long long n_apply = 0, n_explicit = 0, n_restarts = 0, n_block_iters = 0;
+  double t_total = 0, t_spmm = 0, t_ortho = 0, t_lsq = 0, t_comm = 0;
+};
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+double since(Clock::time_point t0) { return std::chrono::duration<double>(Clock::now() - t0).count(); }
+
+struct Problem {  // LinearProblem without preconditioners
+  migmres_solver *S;
+  migmres_crs *A;
+  migmres_mv *X, *B;
+  MvPtr R0;  // PR0 == R0
+  std::vector<int> ls_idx, cur;
+  int ls_num = 0;
+  MvPtr curX, curB;
+
+  void apply(const migmres_mv &x, migmres_mv &y) {
+    auto t0 = Clock::now();
+    crs_apply(*A, x, y, 1.0, 0.0);
+    ++S->n_apply;
+    if (S->p.verbosity & 1) {
+      MIG_HIP(hipStreamSynchronize(A->ctx->stream));
+      S->t_spmm += since(t0);
+    }
+  }
+  void set_problem() {  // setProblem (BelosLinearProblem.hpp:836-946)
+    R0 = MvPtr(mv_create(X->ctx, X->n_global, X->n_local, X->ncols));
+    apply(*X, *R0);
+    mv_add_mv(-1.0, *R0, 1.0, *B, *R0);
+  }
+  void set_ls_index(const std::vector<int> &idx) {  // setLSIndex
+    ls_idx = idx;
+    ++ls_num;
+    cur.clear();
+    for (int i : idx)
+      if (i >= 0) cur.push_back(i);
+    curX = MvPtr(mv_view(X, cur.data(), (int)cur.size()));
+    curB = MvPtr(mv_view(B, cur.data(), (int)cur.size()));
+  }
+  // computeCurrResVec: R = B - A*Xs (BelosLinearProblem.hpp:1196-1231)
+  void curr_res_vec(migmres_mv &R, const migmres_mv *Xs = nullptr) {
+    apply(Xs ? *Xs : *curX, R);
+    mv_add_mv(-1.0, R, 1.0, *curB, R);
+  }
+};
+
+struct ImpResNorm {  // StatusTestImpResNorm, scaling "Norm of Preconditioned Initial Residual"
+  double tol, curr_tol;
+  bool first = true, loss = false, passed = false;
+  int cur_ls_num = 0, numrhs = 0, cur_num_rhs = 0;
+  std::vector<int> cur_idx;
+  std::vector<double> scale, resvector, testvector;
+  MvPtr cur_soln;
+  bool have_soln = false;
+  explicit ImpResNorm(double t) : tol(t), curr_tol(t) {}
+};
+
+struct Iter {  // BlockGmresIter state (keepHessenberg = false: H and R share storage)
+  int k, nb, sd, cur_dim = 0, num_iters = 0;
+  MvPtr V;
+  std::vector<double> R, z, beta, cs, sn;
+  int ldr() const { return sd; }
+  double &Rat(int i, int j) { return R[(size_t)i + (size_t)j * sd]; }
+  double &zat(int i, int j) { return z[(size_t)i + (size_t)j * sd]; }
+};
+
+struct Engine {
+  migmres_solver *S;
+  Problem lp;
+  ImpResNorm imp;
+  int max_iters;
+  int mi_n_iters = 0;
+  bool mi_passed = false;
+
+  Engine(migmres_solver *s, double tol, int mi) : S(s), imp(tol), max_iters(mi) {}
+
+  std::vector<double> native_residuals(Iter &it) {  // getNativeResiduals
+    std::vector<double> r((size_t)it.k);
+    for (int j = 0; j < it.k; ++j) {
+      double s = 0.0, scl = 0.0, ssq = 1.0;
+      for (int i = 0; i < it.k; ++i) {  // dnrm2 scaled sum of squares
+        const double v = it.zat(it.cur_dim + i, j);
+        if (v != 0.0) {
+          const double a = std::fabs(v);
+          if (scl < a) {
+            ssq = 1.0 + ssq * (scl / a) * (scl / a);
+            scl = a;
+          } else {
+            ssq += (a / scl) * (a / scl);
+          }
+        }
+      }
+      s = scl * std::sqrt(ssq);
+      r[(size_t)j] = s;
+    }
+    return r;
+  }
+
+  // getCurrentUpdate (BelosBlockGmresIter.hpp:500-535): TRSM on host, V*y on device.
+  MvPtr current_update(Iter &it) {
+    const int c = it.cur_dim, k = it.k;
+    if (c == 0) return MvPtr();
+    std::vector<double> y((size_t)c * k);
+    for (int j = 0; j < k; ++j)
+      for (int i = 0; i < c; ++i) y[(size_t)i + (size_t)j * c] = it.zat(i, j);
+    for (int j = 0; j < k; ++j)
+      for (int i = c - 1; i >= 0; --i) {
+        double t = y[(size_t)i + (size_t)j * c];
+        for (int q = i + 1; q < c; ++q) t -= it.Rat(i, q) * y[(size_t)q + (size_t)j * c];
+        y[(size_t)i + (size_t)j * c] = t / it.Rat(i, i);
+      }
+    MvPtr upd(mv_create(lp.X->ctx, lp.X->n_global, lp.X->n_local, k));
+    MvPtr Vc = view(*it.V, 0, c);
+    mv_times_mat_add_mv(1.0, *Vc, y.data(), c, 0.0, *upd);
+    return upd;
+  }
+
+  bool max_iters_check(Iter &it) {
+    mi_n_iters = it.num_iters;
+    mi_passed = mi_n_iters >= max_iters;
+    return mi_passed;
+  }
+
+  bool imp_check(Iter &it) {  // StatusTestImpResNorm::checkStatus
+    if (imp.first) {
+      imp.first = false;
+      imp.numrhs = lp.R0->ncols;
+      imp.scale.assign((size_t)imp.numrhs, 0.0);
+      mv_norm(*lp.R0, imp.scale.data(), MIGMRES_TWO_NORM);
+      imp.resvector.assign((size_t)imp.numrhs, 0.0);
+      imp.testvector.assign((size_t)imp.numrhs, 1.0);
+      imp.cur_ls_num = lp.ls_num;
+      imp.cur_idx = lp.ls_idx;
+      imp.cur_num_rhs = 0;
+      for (int i : imp.cur_idx)
+        if (i > -1 && i < imp.numrhs) ++imp.cur_num_rhs;
+    }
+    if (imp.cur_ls_num != lp.ls_num) {
+      imp.cur_ls_num = lp.ls_num;
+      imp.cur_idx = lp.ls_idx;
+      imp.cur_num_rhs = 0;
+      for (int i : imp.cur_idx)
+        if (i > -1 && i < imp.numrhs) ++imp.cur_num_rhs;
+      imp.have_soln = false;
+    } else if (imp.passed) {
+      return true;
+    }
+    auto res = native_residuals(it);
+    for (size_t i = 0; i < imp.cur_idx.size(); ++i)
+      if (imp.cur_idx[i] != -1) imp.resvector[(size_t)imp.cur_idx[i]] = res[i];
+    for (int p : imp.cur_idx)
+      if (p != -1) {
+        const double s = imp.scale[(size_t)p];
+        imp.testvector[(size_t)p] = s != 0.0 ? imp.resvector[(size_t)p] / s / 1.0 : imp.resvector[(size_t)p] / 1.0;
+      }
+    std::vector<int> ind, lcl;
+    for (size_t i = 0; i < imp.cur_idx.size(); ++i) {
+      const int p = imp.cur_idx[i];
+      if (p == -1) continue;
+      const double tv = imp.testvector[(size_t)p];
+      if (tv > imp.curr_tol) {
+      } else if (tv <= imp.curr_tol) {
+        ind.push_back(p);
+        lcl.push_back((int)i);
+      } else {
+        throw Error(MIGMRES_ESTATE, "StatusTestImpResNorm: implicit residual norm is NaN");
+      }
+    }
+    int have = (int)ind.size();
+    if (have) {
+      ++S->n_explicit;
+      MvPtr upd = current_update(it);
+      const int k = lp.curX->ncols;
+      if (!imp.cur_soln.p || imp.cur_soln->ncols != k)
+        imp.cur_soln = MvPtr(mv_create(lp.X->ctx, lp.X->n_global, lp.X->n_local, k));
+      if (upd.p)
+        mv_add_mv(1.0, *lp.curX, 1.0, *upd, *imp.cur_soln);
+      else
+        mv_assign(*lp.curX, *imp.cur_soln);
+      imp.have_soln = true;
+      MvPtr cur_res(mv_create(lp.X->ctx, lp.X->n_global, lp.X->n_local, k));
+      lp.curr_res_vec(*cur_res, imp.cur_soln.p);
+      std::vector<double> tmp_res((size_t)k);
+      mv_norm(*cur_res, tmp_res.data(), MIGMRES_TWO_NORM);
+      std::vector<double> tmp_test((size_t)have);
+      for (int i = 0; i < have; ++i) {
+        const double s = imp.scale[(size_t)ind[(size_t)i]];
+        tmp_test[(size_t)i] = s != 0.0 ? tmp_res[(size_t)lcl[(size_t)i]] / s / 1.0 : tmp_res[(size_t)lcl[(size_t)i]] / 1.0;
+      }
+      int have2 = 0;
+      for (int i = 0; i < have; ++i) {
+        if (tmp_test[(size_t)i] <= imp.tol) {
+          ind[(size_t)have2++] = ind[(size_t)i];
+        } else {
+          const double diff = std::fabs(imp.testvector[(size_t)ind[(size_t)i]] - tmp_test[(size_t)i]);
+          if (diff > imp.curr_tol) {
+            imp.loss = true;
+            ind[(size_t)have2++] = ind[(size_t)i];
+          } else {
+            imp.curr_tol = imp.curr_tol - (3.0 / 2.0) * diff;
+            while (imp.curr_tol < 0.0) imp.curr_tol += (1.0 / 10.0) * diff;
+          }
+        }
+      }
+      have = have2;
+    }
+    imp.passed = have >= imp.cur_num_rhs;
+    return imp.passed;
+  }
+
+  bool check(Iter &it) {  // StatusTestCombo OR: both members evaluated
+    const bool a = max_iters_check(it);
+    const bool b = imp_check(it);
+    S->history.insert(S->history.end(), imp.testvector.begin(), imp.testvector.end());
+    S->hist_cols = (int)imp.testvector.size();
+    return a || b;
+  }
+
+  void initialize(Iter &it, migmres_mv &V0, const std::vector<double> &z0) {  // initializeGmres
+    const int k = it.k;
+    it.cur_dim = 0;
+    MvPtr v = view(*it.V, 0, k);
+    mv_add_mv(1.0, V0, 0.0, V0, *v);
+    std::fill(it.z.begin(), it.z.end(), 0.0);
+    for (int j = 0; j < k; ++j)
+      for (int i = 0; i < k; ++i) it.zat(i, j) = z0[(size_t)i + (size_t)j * k];
+  }
+
+  void update_lsqr(Iter &it, int dim = -1) {  // updateLSQR (BelosBlockGmresIter.hpp:770-868)
+    auto t0 = Clock::now();
+    const int k = it.k;
+    int cur = it.cur_dim;
+    if (dim >= it.cur_dim && dim < k * it.nb) cur = dim;
+    if (k == 1) {
+      for (int i = 0; i < cur; ++i) {
+        const double x = it.Rat(i, cur), y = it.Rat(i + 1, cur);
+        it.Rat(i, cur) = it.cs[(size_t)i] * x + it.sn[(size_t)i] * y;
+        it.Rat(i + 1, cur) = it.cs[(size_t)i] * y - it.sn[(size_t)i] * x;
+      }
+      rotg(it.Rat(cur, cur), it.Rat(cur + 1, cur), it.cs[(size_t)cur], it.sn[(size_t)cur]);
+      it.Rat(cur + 1, cur) = 0.0;
+      const double x = it.zat(cur, 0), y = it.zat(cur + 1, 0);
+      it.zat(cur, 0) = it.cs[(size_t)cur] * x + it.sn[(size_t)cur] * y;
+      it.zat(cur + 1, 0) = it.cs[(size_t)cur] * y - it.sn[(size_t)cur] * x;
+    } else {
+      for (int j = 0; j < k; ++j) {
+        const int cj = cur + j;
+        for (int i = 0; i < cj; ++i) {
+          double sigma = 0.0;
+          for (int q = 0; q < k; ++q) sigma += it.Rat(i + 1 + q, i) * it.Rat(i + 1 + q, cj);
+          sigma += it.Rat(i, cj);
+          sigma *= it.beta[(size_t)i];
+          for (int q = 0; q < k; ++q) it.Rat(i + 1 + q, cj) += (-sigma) * it.Rat(i + 1 + q, i);
+          it.Rat(i, cj) -= sigma;
+        }
+        int maxidx = 0;
+        double maxabs = -1.0;
+        for (int q = 0; q < k + 1; ++q) {
+          const double a = std::fabs(it.Rat(cj + q, cj));
+          if (a > maxabs) {
+            maxabs = a;
+            maxidx = q;
+          }
+        }
+        const double maxelem = it.Rat(cj + maxidx, cj);
+        for (int q = 0; q < k + 1; ++q) it.Rat(cj + q, cj) /= maxelem;
+        double sigma = 0.0;
+        for (int q = 0; q < k; ++q) sigma += it.Rat(cj + 1 + q, cj) * it.Rat(cj + 1 + q, cj);
+        if (sigma == 0.0) {
+          it.beta[(size_t)cj] = 0.0;
+        } else {
+          const double d = it.Rat(cj, cj);
+          const double mu = std::sqrt(d * d + sigma);
+          const double vscale = d < 0.0 ? d - mu : -sigma / (d + mu);
+          it.beta[(size_t)cj] = 2.0 * 1.0 * vscale * vscale / (sigma + vscale * vscale);
+          it.Rat(cj, cj) = maxelem * mu;
+          for (int q = 0; q < k; ++q) it.Rat(cj + 1 + q, cj) /= vscale;
+        }
+        for (int col = 0; col < k; ++col) {
+          double s2 = 0.0;
+          for (int q = 0; q < k; ++q) s2 += it.Rat(cj + 1 + q, cj) * it.zat(cj + 1 + q, col);
+          s2 += it.zat(cj, col);
+          s2 *= it.beta[(size_t)cj];
+          for (int q = 0; q < k; ++q) it.zat(cj + 1 + q, col) += (-s2) * it.Rat(cj + 1 + q, cj);
+          it.zat(cj, col) -= s2;
+        }
+      }
+    }
+    if (dim >= it.cur_dim && dim < k * it.nb) it.cur_dim = dim + k;
+    S->t_lsq += since(t0);
+  }
+
+  struct OrthoFailure {};
+
+  void iterate(Iter &it) {  // BlockGmresIter::iterate (BelosBlockGmresIter.hpp:659-766)
+    const int k = it.k, search = k * it.nb;
+    std::vector<double> subH, subH2;
+    while (!check(it) && it.cur_dim + k <= search) {
+      ++it.num_iters;
+      ++S->n_block_iters;
+      const int lcl = it.cur_dim + k, c = it.cur_dim;
+      MvPtr Vnext = view(*it.V, lcl, k);
+      MvPtr Vprev = view(*it.V, c, k);
+      lp.apply(*Vprev, *Vnext);
+      MvPtr Q = view(*it.V, 0, lcl);
+      subH.assign((size_t)lcl * k, 0.0);
+      subH2.assign((size_t)k * k, 0.0);
+      auto t0 = Clock::now();
+      const int rank = S->ortho.project_and_normalize(*Vnext, *Q, subH.data(), lcl, subH2.data(), k);
+      S->t_ortho += since(t0);
+      for (int j = 0; j < k; ++j) {
+        for (int i = 0; i < lcl; ++i) it.Rat(i, c + j) = subH[(size_t)i + (size_t)j * lcl];
+        for (int i = 0; i < k; ++i) it.Rat(lcl + i, c + j) = subH2[(size_t)i + (size_t)j * k];
+      }
+      if (rank != k) throw OrthoFailure{};
+      update_lsqr(it);
+      it.cur_dim += k;
+    }
+  }
+
+  // BlockGmresSolMgr::solve (BelosBlockGmresSolMgr.hpp:916-1303), non-flexible.
+  bool solve() {
+    const Params &p = S->p;
+    int block = p.block_size;
+    const int numrhs = lp.B->ncols;
+    int start = 0, to_solve = numrhs;
+    int cur_rhs = std::min(to_solve, block);
+    std::vector<int> idx;
+    auto make_idx = [&]() {
+      idx.clear();
+      if (p.adaptive) {
+        block = cur_rhs;
+        for (int i = 0; i < cur_rhs; ++i) idx.push_back(start + i);
+      } else {
+        for (int i = 0; i < cur_rhs; ++i) idx.push_back(start + i);
+        for (int i = cur_rhs; i < block; ++i) idx.push_back(-1);
+      }
+    };
+    make_idx();
+    lp.set_ls_index(idx);
+    const long long dim = lp.B->n_global;
+    bool converged = true;
+    S->loa = false;
+    while (to_solve > 0) {
+      int nb = p.num_blocks;
+      if ((long long)block * p.num_blocks > dim) nb = (int)(block == 1 ? dim / block : (dim - block) / block);
+      Iter it;
+      it.k = block;
+      it.nb = nb;
+      it.sd = block * (nb + 1);
+      it.V = MvPtr(mv_create(lp.X->ctx, lp.X->n_global, lp.X->n_local, it.sd));
+      it.R.assign((size_t)it.sd * (it.sd - block), 0.0);
+      it.z.assign((size_t)it.sd * block, 0.0);
+      it.beta.assign((size_t)it.sd, 0.0);
+      it.cs.assign((size_t)it.sd, 0.0);
+      it.sn.assign((size_t)it.sd, 0.0);
+      MvPtr V0(mv_create(lp.X->ctx, lp.X->n_global, lp.X->n_local, block));
+      if (idx.back() == -1)
+        lp.curr_res_vec(*V0);
+      else {
+        MvPtr r0v(mv_view(lp.R0.p, idx.data(), (int)idx.size()));
+        mv_assign(*r0v, *V0);
+      }
+      std::vector<double> z0((size_t)block * block, 0.0);
+      if (S->ortho.normalize(*V0, z0.data(), block) != block)
+        throw Error(MIGMRES_ESTATE, "BlockGmresSolMgr: failed to compute initial block of orthonormal vectors");
+      initialize(it, *V0, z0);
+      int restarts = 0;
+      while (true) {
+        try {
+          iterate(it);
+          if (imp.passed) {
+            if (imp.loss) {
+              S->loa = true;
+              converged = false;
+            }
+            break;
+          } else if (mi_passed) {
+            converged = false;
+            break;
+          } else if (it.cur_dim == it.k * it.nb) {
+            if (restarts >= p.max_restarts) {
+              converged = false;
+              break;
+            }
+            ++restarts;
+            MvPtr upd = current_update(it);
+            if (upd.p) mv_add_mv(1.0, *lp.curX, 1.0, *upd, *lp.curX);
+            lp.curr_res_vec(*V0);
+            std::fill(z0.begin(), z0.end(), 0.0);
+            if (S->ortho.normalize(*V0, z0.data(), block) != block)
+              throw Error(MIGMRES_ESTATE, "BlockGmresSolMgr: failed to compute initial block after restart");
+            initialize(it, *V0, z0);
+          } else {
+            throw Error(MIGMRES_ESTATE, "BlockGmresSolMgr: invalid return from iterate()");
+          }
+        } catch (const OrthoFailure &) {
+          if (block != 1) {
+            if (!imp.passed) converged = false;
+            break;
+          }
+          update_lsqr(it, it.cur_dim);
+          check(it);
+          if (!imp.passed) converged = false;
+          break;
+        }
+      }
+      if (imp.have_soln) {
+        mv_assign(*imp.cur_soln, *lp.curX);
+      } else {
+        MvPtr upd = current_update(it);
+        if (upd.p) mv_add_mv(1.0, *lp.curX, 1.0, *upd, *lp.curX);
+      }
+      S->n_restarts += restarts;
+      start += cur_rhs;
+      to_solve -= cur_rhs;
+      if (to_solve > 0) {
+        cur_rhs = std::min(to_solve, block);
+        make_idx();
+        lp.set_ls_index(idx);
+      }
+    }
+    MIG_HIP(hipStreamSynchronize(lp.X->ctx->stream));
+    S->num_iters = mi_n_iters;
+    S->achieved_tol = imp.testvector.empty() ? 0.0 : *std::max_element(imp.testvector.begin(), imp.testvector.end());
+    return converged && !S->loa;
+  }
+};
+
+}  // namespace
+
+
+extern "C" int migmres_solver_create(migmres_ctx *ctx, migmres_solver **out) {
+  return guard([&] {
+    MIG_CHECK(ctx && out, "bad solver arguments");
+    auto *s = new migmres_solver();
+    s->ctx = ctx;
+    *out = s;
+  });
+}
+
+extern "C" int migmres_solver_destroy(migmres_solver *s) {
+  return guard([&] { delete s; });
+}
+
+extern "C" int migmres_solver_set_int(migmres_solver *s, const char *name, long long v) {
+  return guard([&] {
+    const std::string n(name);
+    if (n == "Block Size") {
+      MIG_CHECK(v > 0, "\"Block Size\" must be strictly positive");
+      s->p.block_size = (int)v;
+    } else if (n == "Num Blocks") {
+      MIG_CHECK(v > 0, "\"Num Blocks\" must be strictly positive");
+      s->p.num_blocks = (int)v;
+    } else if (n == "Maximum Iterations") {
+      s->p.max_iters = (int)v;
+    } else if (n == "Maximum Restarts") {
+      s->p.max_restarts = (int)v;
+    } else if (n == "Adaptive Block Size") {
+      s->p.adaptive = v != 0;
+    } else if (n == "Verbosity") {
+      s->p.verbosity = (int)v;
+    } else if (n == "Output Frequency") {
+      s->p.output_freq = (int)v;
+    } else {
+      throw Error(MIGMRES_EINVAL, "unknown integer parameter \"" + n + "\"");
+    }
+  });
+}
+
+extern "C" int migmres_solver_set_double(migmres_solver *s, const char *name, double v) {
+  return guard([&] {
+    const std::string n(name);
+    if (n == "Convergence Tolerance")
+      s->p.tol = v;
+    else
+      throw Error(MIGMRES_EINVAL, "unknown double parameter \"" + n + "\"");
+  });
+}
+
+extern "C" int migmres_solver_set_string(migmres_solver *s, const char *name, const char *v) {
+  return guard([&] {
+    const std::string n(name), val(v);
+    if (n == "Orthogonalization") {
+      MIG_CHECK(val == "DGKS" || val == "ICGS" || val == "IMGS",
+                "\"Orthogonalization\" must be either \"DGKS\", \"ICGS\", or \"IMGS\"");
+      MIG_CHECK(val == "ICGS", "only \"ICGS\" is implemented on the device path");
+      s->p.ortho = val;
+    } else if (n == "Implicit Residual Scaling") {
+      MIG_CHECK(val == "Norm of Preconditioned Initial Residual", "only the default implicit scaling is supported");
+    } else {
+      throw Error(MIGMRES_EINVAL, "unknown string parameter \"" + n + "\"");
+    }
+  });
+}
+
+extern "C" int migmres_solver_solve(migmres_solver *s, migmres_crs *A, migmres_mv *X,
+                                    const migmres_mv *B, int *converged) {
+  return guard([&] {
+    MIG_CHECK(s && A && X && B, "bad solve arguments");
+    MIG_CHECK(s->p.ortho == "ICGS", "set \"Orthogonalization\" to \"ICGS\"");
+    MIG_CHECK(X->ncols == B->ncols && X->n_local == A->n_local && B->n_local == A->n_local,
+              "LinearProblem: inconsistent X/B/A shapes");
+    s->history.clear();
+    s->n_apply = s->n_explicit = s->n_restarts = s->n_block_iters = 0;
+    s->t_spmm = s->t_ortho = s->t_lsq = 0.0;
+    const double comm0 = s->ctx->comm_seconds;
+    auto t0 = Clock::now();
+    Engine E(s, s->p.tol, s->p.max_iters);
+    E.lp.S = s;
+    E.lp.A = A;
+    E.lp.X = X;
+    E.lp.B = const_cast<migmres_mv *>(B);
+    E.lp.set_problem();
+    const bool ok = E.solve();
+    s->t_total = since(t0);
+    s->t_comm = s->ctx->comm_seconds - comm0;
+    if (converged) *converged = ok ? 1 : 0;
+  });
+}
+
+extern "C" int migmres_solver_num_iters(const migmres_solver *s, int *it) {
+  return guard([&] { *it = s->num_iters; });
+}
+extern "C" int migmres_solver_achieved_tol(const migmres_solver *s, double *tol) {
+  return guard([&] { *tol = s->achieved_tol; });
+}
+extern "C" int migmres_solver_loa_detected(const migmres_solver *s, int *loa) {
+  return guard([&] { *loa = s->loa ? 1 : 0; });
+}
+extern "C" int migmres_solver_history(const migmres_solver *s, double *out, int *nrows, int *ncols) {
+  return guard([&] {
+    const int nc = s->hist_cols > 0 ? s->hist_cols : 1;
+    *ncols = s->hist_cols;
+    *nrows = s->hist_cols > 0 ? (int)(s->history.size() / nc) : 0;
+    if (out) std::memcpy(out, s->history.data(), sizeof(double) * s->history.size());
+  });
+}
+extern "C" int migmres_solver_counters(const migmres_solver *s, long long *out, int n) {
+  return guard([&] {
+    const long long v[5] = {s->n_apply, s->n_explicit, s->n_restarts, s->ortho.sing_count, s->n_block_iters};
+    for (int i = 0; i < n && i < 5; ++i) out[i] = v[i];
+  });
+}
+extern "C" int migmres_solver_timers(const migmres_solver *s, double *out, int n) {
+  return guard([&] {
+    const double v[5] = {s->t_total, s->t_spmm, s->t_ortho, s->t_lsq, s->t_comm};
+    for (int i = 0; i < n && i < 5; ++i) out[i] = v[i];
+  });
+}
+
+// ICGS entry points on caller-provided multivectors (the OrthoManager drop-in).
+static Icgs g_icgs_default;
+extern "C" int migmres_icgs_project_normalize(migmres_mv *X, const migmres_mv *Q, double *C, int ldc,
+                                              double *B, int ldb, int *rank) {
+  return guard([&] {
+    MIG_CHECK(X && Q && rank, "bad ICGS arguments");
+    *rank = g_icgs_default.project_and_normalize(*X, *const_cast<migmres_mv *>(Q), C, ldc, B, ldb);
+  });
+}
+extern "C" int migmres_icgs_normalize(migmres_mv *X, double *B, int ldb, int *rank) {
+  return guard([&] {
+    MIG_CHECK(X && rank, "bad ICGS arguments");
+    *rank = g_icgs_default.normalize(*X, B, ldb);
+    MIG_HIP(hipStreamSynchronize(X->ctx->stream));
+  });
+}
