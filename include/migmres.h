@@ -71,6 +71,13 @@ int migmres_ctx_rank(const migmres_ctx *ctx, int *rank, int *nranks);
 /* Sum-all of n host doubles across ranks (Epetra_Comm::SumAll). */
 int migmres_ctx_sum_all(migmres_ctx *ctx, const double *in, double *out, int n);
 
+/* Kernel profiling with HIP events on the context stream: per kernel class the summed
+ * device milliseconds, ALGORITHMIC bytes (the traffic model of DESIGN.md) and launch
+ * count.  Enabling resets the counters.  Class names: migmres_kernel_class_name(i). */
+int migmres_ctx_profile(migmres_ctx *ctx, int on);
+int migmres_ctx_profile_read(migmres_ctx *ctx, double *ms, double *bytes, long long *launches, int n);
+const char *migmres_kernel_class_name(int i);
+
 /* ---------------- maps and import plans (host only, no GPU needed) ---------------- */
 
 /* Epetra_BlockMap::ConstructAutoUniform: first global id and local length of `rank`. */

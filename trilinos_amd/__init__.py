@@ -1,0 +1,17 @@
+"""trilinos_amd -- an MI355X-native (gfx950) Block GMRES hot path with the Belos/Epetra
+interface shape.
+
+The product is ``libmigmres.so`` (HIP kernels + host C++ solver behind the C ABI in
+``include/migmres.h``); this package is the Python mirror of the reference's
+operator/solver interface over that ABI.  Importing it loads the library and fails
+loudly if it has not been built -- there is no CPU fallback.
+"""
+
+from . import _lib  # noqa: F401  (raises ImportError when libmigmres.so is missing)
+from .linalg import Comm, CrsMatrix, MultiVector, uniform_map  # noqa: F401
+from .belos import (BlockGmresSolMgr, ICGSOrthoManager, LinearProblem, MultiVecTraits,  # noqa: F401
+                    OperatorTraits, Converged, Unconverged, TwoNorm, OneNorm, InfNorm)
+
+__all__ = ["Comm", "CrsMatrix", "MultiVector", "uniform_map", "BlockGmresSolMgr",
+           "ICGSOrthoManager", "LinearProblem", "MultiVecTraits", "OperatorTraits",
+           "Converged", "Unconverged", "TwoNorm", "OneNorm", "InfNorm"]

@@ -1,0 +1,306 @@
+"""Belos solver-layer mirror over the C ABI.
+
+  MultiVecTraits     Belos::MultiVecTraits<double,MV> (belos/src/BelosMultiVecTraits.hpp:138-347,
+                     Epetra specialisation belos/epetra/src/BelosEpetraAdapter.hpp:447-1064)
+  OperatorTraits     Belos::OperatorTraits<double,MV,OP> (belos/src/BelosOperatorTraits.hpp:108-155)
+  ICGSOrthoManager   Belos::ICGSOrthoManager (belos/src/BelosICGSOrthoManager.hpp:646-839)
+  LinearProblem      Belos::LinearProblem (belos/src/BelosLinearProblem.hpp)
+  BlockGmresSolMgr   Belos::BlockGmresSolMgr (belos/src/BelosBlockGmresSolMgr.hpp)
+
+Same names, argument meaning and error behaviour as the reference; the N-sized work runs
+in HIP kernels, the control flow in the C++ solver behind include/migmres.h.
+"""
+
+import ctypes as C
+
+import numpy as np
+
+from ._lib import call, dptr, iptr
+from .linalg import MultiVector, TWO_NORM, ONE_NORM, INF_NORM  # noqa: F401
+
+Converged, Unconverged = "Converged", "Unconverged"  # Belos::ReturnType (BelosTypes.hpp:155-157)
+TwoNorm, OneNorm, InfNorm = TWO_NORM, ONE_NORM, INF_NORM
+
+
+class MultiVecTraits:
+    """Static MVT interface.  Dense coefficient matrices are numpy arrays (column-major
+    Teuchos::SerialDenseMatrix semantics); results that the reference returns in a
+    SerialDenseMatrix / std::vector are returned as numpy arrays."""
+
+    @staticmethod
+    def Clone(mv, numvecs):
+        return MultiVector(mv.comm, mv.n_global, numvecs)
+
+    @staticmethod
+    def CloneCopy(mv, index=None):
+        src = mv if index is None else mv.view(index)
+        out = MultiVector(mv.comm, mv.n_global, src.ncols)
+        call("migmres_mv_assign", src.h, out.h)
+        return out
+
+    @staticmethod
+    def CloneView(mv, index):
+        return mv.view(index)
+
+    CloneViewNonConst = CloneView
+
+    @staticmethod
+    def GetGlobalLength(mv):
+        return mv.n_global
+
+    @staticmethod
+    def GetNumberVecs(mv):
+        return mv.ncols
+
+    @staticmethod
+    def HasConstantStride(mv):
+        return mv.constant_stride
+
+    @staticmethod
+    def MvTimesMatAddMv(alpha, A, B, beta, mv):
+        B = np.asfortranarray(B, dtype=np.float64)
+        if B.shape != (A.ncols, mv.ncols):
+            raise ValueError("MvTimesMatAddMv: B must be A.ncols x mv.ncols")
+        call("migmres_mv_times_mat_add_mv", float(alpha), A.h, dptr(B), max(B.shape[0], 1),
+             float(beta), mv.h)
+
+    @staticmethod
+    def MvAddMv(alpha, A, beta, B, mv):
+        call("migmres_mv_add_mv", float(alpha), A.h, float(beta), B.h, mv.h)
+
+    @staticmethod
+    def MvScale(mv, alpha):
+        if np.ndim(alpha) == 0:
+            call("migmres_mv_scale", mv.h, float(alpha))
+        else:
+            a = np.ascontiguousarray(alpha, dtype=np.float64)
+            if a.size != mv.ncols:
+                raise ValueError("MvScale: one scaling coefficient per column")
+            call("migmres_mv_scale_vec", mv.h, dptr(a))
+
+    @staticmethod
+    def MvTransMv(alpha, A, mv):
+        """C = alpha * A^T mv, replicated on every rank."""
+        Cm = np.zeros((A.ncols, mv.ncols), dtype=np.float64, order="F")
+        call("migmres_mv_trans_mv", float(alpha), A.h, mv.h, dptr(Cm), max(A.ncols, 1))
+        return Cm
+
+    @staticmethod
+    def MvDot(mv, A):
+        out = np.zeros(mv.ncols)
+        call("migmres_mv_dot", mv.h, A.h, dptr(out))
+        return out
+
+    @staticmethod
+    def MvNorm(mv, type=TwoNorm):
+        out = np.zeros(mv.ncols)
+        call("migmres_mv_norm", mv.h, dptr(out), int(type))
+        return out
+
+    @staticmethod
+    def SetBlock(A, index, mv):
+        idx = np.ascontiguousarray(index, dtype=np.int32)
+        call("migmres_mv_set_block", A.h, iptr(idx), idx.size, mv.h)
+
+    @staticmethod
+    def Assign(A, mv):
+        call("migmres_mv_assign", A.h, mv.h)
+
+    @staticmethod
+    def MvRandom(mv, seed=1):
+        return mv.random(seed)
+
+    @staticmethod
+    def MvInit(mv, alpha=0.0):
+        mv.put_scalar(alpha)
+
+    @staticmethod
+    def MvPrint(mv):
+        return str(mv.download())
+
+
+class OperatorTraits:
+    @staticmethod
+    def Apply(Op, x, y, trans=False):
+        if trans:
+            raise NotImplementedError("transpose apply is not on the hot path")
+        Op.apply(x, y)
+
+    @staticmethod
+    def HasApplyTranspose(Op):
+        return False
+
+
+class ICGSOrthoManager:
+    """projectAndNormalize / normalize with the reference defaults (2 passes,
+    blk_tol = 10 sqrt(eps), sing_tol = 10 eps)."""
+
+    def projectAndNormalize(self, X, Q):
+        """Returns (rank, C, B) with C = (Q.ncols x X.ncols), B = (X.ncols x X.ncols)."""
+        Cm = np.zeros((Q.ncols, X.ncols), order="F")
+        Bm = np.zeros((X.ncols, X.ncols), order="F")
+        r = C.c_int()
+        call("migmres_icgs_project_normalize", X.h, Q.h, dptr(Cm), max(Q.ncols, 1), dptr(Bm),
+             max(X.ncols, 1), C.byref(r))
+        return r.value, Cm, Bm
+
+    def normalize(self, X):
+        Bm = np.zeros((X.ncols, X.ncols), order="F")
+        r = C.c_int()
+        call("migmres_icgs_normalize", X.h, dptr(Bm), max(X.ncols, 1), C.byref(r))
+        return r.value, Bm
+
+
+class LinearProblem:
+    """Belos::LinearProblem(A, X, B) without preconditioners."""
+
+    def __init__(self, A, X, B):
+        self.A, self.X, self.B = A, X, B
+        self._set = False
+
+    def setProblem(self):
+        if self.X is None or self.B is None or self.A is None:
+            return False
+        if self.X.ncols != self.B.ncols:
+            return False
+        self._set = True
+        return True
+
+    def isProblemSet(self):
+        return self._set
+
+
+_INT_PARAMS = {"Block Size", "Num Blocks", "Maximum Iterations", "Maximum Restarts", "Verbosity",
+               "Output Frequency"}
+_BOOL_PARAMS = {"Adaptive Block Size"}
+_DOUBLE_PARAMS = {"Convergence Tolerance"}
+_STRING_PARAMS = {"Orthogonalization", "Implicit Residual Scaling"}
+
+# BelosBlockGmresSolMgr.hpp:323-338 and DefaultSolverParameters::convTol
+DEFAULT_PARAMETERS = {
+    "Convergence Tolerance": 1e-8, "Maximum Restarts": 20, "Maximum Iterations": 1000,
+    "Num Blocks": 300, "Block Size": 1, "Adaptive Block Size": True, "Verbosity": 0,
+    "Output Frequency": -1, "Orthogonalization": "DGKS",
+    "Implicit Residual Scaling": "Norm of Preconditioned Initial Residual",
+}
+
+
+class BlockGmresSolMgr:
+    """Belos::BlockGmresSolMgr over the device solver.
+
+    Parameters use the reference ParameterList names.  Only the "ICGS"
+    orthogonalization is implemented on the device path; setting "DGKS" or "IMGS"
+    raises at solve() (the reference default "DGKS" is listed in SURVEY.md 8(f) as next).
+    """
+
+    def __init__(self, problem=None, params=None):
+        self.problem = problem
+        self.params = dict(DEFAULT_PARAMETERS)
+        h = C.c_void_p()
+        self.comm = None
+        self.h = None
+        self._pending = {}
+        if params:
+            self.setParameters(params)
+
+    def _ensure(self):
+        if self.h is None:
+            if self.problem is None:
+                raise RuntimeError("BlockGmresSolMgr: no LinearProblem set")
+            self.comm = self.problem.A.comm
+            h = C.c_void_p()
+            call("migmres_solver_create", self.comm.h, C.byref(h))
+            self.h = h
+            for k, v in self.params.items():
+                self._push(k, v)
+
+    def _push(self, name, v):
+        n = name.encode()
+        if name in _INT_PARAMS:
+            call("migmres_solver_set_int", self.h, n, int(v))
+        elif name in _BOOL_PARAMS:
+            call("migmres_solver_set_int", self.h, n, 1 if v else 0)
+        elif name in _DOUBLE_PARAMS:
+            call("migmres_solver_set_double", self.h, n, float(v))
+        elif name in _STRING_PARAMS:
+            if name == "Orthogonalization" and v not in ("DGKS", "ICGS", "IMGS"):
+                raise ValueError('"Orthogonalization" must be either "DGKS", "ICGS", or "IMGS".')
+            if name == "Orthogonalization" and v != "ICGS":
+                return  # validated at solve()
+            call("migmres_solver_set_string", self.h, n, str(v).encode())
+
+    def setProblem(self, problem):
+        self.problem = problem
+
+    def getValidParameters(self):
+        return dict(DEFAULT_PARAMETERS)
+
+    def setParameters(self, params):
+        for k, v in params.items():
+            if k not in DEFAULT_PARAMETERS:
+                raise KeyError(f'"{k}" is not a valid BlockGmresSolMgr parameter')
+            if k == "Block Size" and int(v) <= 0:
+                raise ValueError('"Block Size" must be strictly positive.')
+            if k == "Num Blocks" and int(v) <= 0:
+                raise ValueError('"Num Blocks" must be strictly positive.')
+            if k == "Orthogonalization" and v not in ("DGKS", "ICGS", "IMGS"):
+                raise ValueError('"Orthogonalization" must be either "DGKS", "ICGS", or "IMGS".')
+            self.params[k] = v
+            if self.h is not None:
+                self._push(k, v)
+
+    def getCurrentParameters(self):
+        return dict(self.params)
+
+    def solve(self):
+        if self.problem is None or not self.problem.isProblemSet():
+            raise RuntimeError("BlockGmresSolMgr::solve(): Linear problem is not ready, "
+                               "setProblem() has not been called.")
+        if self.params["Orthogonalization"] != "ICGS":
+            raise NotImplementedError('device Block GMRES implements "Orthogonalization" = "ICGS"')
+        self._ensure()
+        conv = C.c_int()
+        call("migmres_solver_solve", self.h, self.problem.A.h, self.problem.X.h,
+             self.problem.B.h, C.byref(conv))
+        return Converged if conv.value else Unconverged
+
+    def getNumIters(self):
+        v = C.c_int()
+        call("migmres_solver_num_iters", self.h, C.byref(v))
+        return v.value
+
+    def achievedTol(self):
+        v = C.c_double()
+        call("migmres_solver_achieved_tol", self.h, C.byref(v))
+        return v.value
+
+    def isLOADetected(self):
+        v = C.c_int()
+        call("migmres_solver_loa_detected", self.h, C.byref(v))
+        return bool(v.value)
+
+    def residualHistory(self):
+        nr, nc = C.c_int(), C.c_int()
+        call("migmres_solver_history", self.h, None, C.byref(nr), C.byref(nc))
+        out = np.zeros(max(nr.value * nc.value, 1))
+        call("migmres_solver_history", self.h, dptr(out), C.byref(nr), C.byref(nc))
+        return out[:nr.value * nc.value].reshape(nr.value, nc.value)
+
+    def counters(self):
+        out = (C.c_longlong * 5)()
+        call("migmres_solver_counters", self.h, out, 5)
+        keys = ("applies", "explicit_checks", "restarts", "blk_ortho_sing", "block_iterations")
+        return dict(zip(keys, list(out)))
+
+    def timers(self):
+        out = (C.c_double * 5)()
+        call("migmres_solver_timers", self.h, out, 5)
+        keys = ("total", "spmm", "ortho", "lsqr", "comm")
+        return dict(zip(keys, list(out)))
+
+    def __del__(self):
+        try:
+            if self.h is not None:
+                call("migmres_solver_destroy", self.h)
+        except Exception:
+            pass

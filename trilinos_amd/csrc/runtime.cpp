@@ -58,6 +58,78 @@ void migmres_ctx::allreduce(double *d, size_t n, bool max) {
   comm_seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
 
+const char *kKernelClassNames[K_NUM_CLASSES] = {"spmm", "gemm_tn", "reduce", "gemm_nn", "coldot",
+                                                "axpby", "scale", "fill", "copy", "random", "pack"};
+
+hipEvent_t migmres_ctx::get_event() {
+  if (!event_pool.empty()) {
+    hipEvent_t e = event_pool.back();
+    event_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  MIG_HIP(hipEventCreate(&e));
+  return e;
+}
+
+void migmres_ctx::prof_collect() {
+  if (pending.empty()) return;
+  MIG_HIP(hipStreamSynchronize(stream));
+  for (auto &p : pending) {
+    float ms = 0.f;
+    MIG_HIP(hipEventElapsedTime(&ms, p.a, p.b));
+    prof_ms[p.cls] += ms;
+    prof_bytes[p.cls] += p.bytes;
+    prof_count[p.cls] += 1;
+    event_pool.push_back(p.a);
+    event_pool.push_back(p.b);
+  }
+  pending.clear();
+}
+
+ProfScope::ProfScope(migmres_ctx *ctx, int k, double by) : c(ctx), cls(k), bytes(by) {
+  if (!c->prof_on) return;
+  a = c->get_event();
+  b = c->get_event();
+  MIG_HIP(hipEventRecord(a, c->stream));
+}
+
+ProfScope::~ProfScope() {
+  if (!c->prof_on || !a) return;
+  hipEventRecord(b, c->stream);
+  c->pending.push_back({cls, bytes, a, b});
+  if (c->pending.size() > 2048) {
+    try {
+      c->prof_collect();
+    } catch (...) {
+    }
+  }
+}
+
+extern "C" int migmres_ctx_profile(migmres_ctx *c, int on) {
+  return guard([&] {
+    c->prof_collect();
+    c->prof_on = on != 0;
+    for (int i = 0; i < K_NUM_CLASSES; ++i) c->prof_ms[i] = c->prof_bytes[i] = 0.0, c->prof_count[i] = 0;
+  });
+}
+
+extern "C" int migmres_ctx_profile_read(migmres_ctx *c, double *ms, double *bytes, long long *launches,
+                                        int n) {
+  return guard([&] {
+    c->prof_collect();
+    for (int i = 0; i < n && i < K_NUM_CLASSES; ++i) {
+      ms[i] = c->prof_ms[i];
+      bytes[i] = c->prof_bytes[i];
+      launches[i] = c->prof_count[i];
+    }
+  });
+}
+
+extern "C" const char *migmres_kernel_class_name(int i) {
+  return (i >= 0 && i < K_NUM_CLASSES) ? kKernelClassNames[i] : "";
+}
+
 extern "C" int migmres_comm_unique_id(unsigned char out[128]) {
   return guard([&] {
     ncclUniqueId id;
@@ -212,7 +284,10 @@ void mv_times_mat_add_mv(double alpha, const migmres_mv &A, const double *B, int
     for (int i = 0; i < L; ++i) h[(size_t)i + (size_t)j * L] = B[(size_t)i + (size_t)j * ldb];
   double *d = c->coef((size_t)L * k);
   MIG_HIP(hipMemcpyAsync(d, h, sizeof(double) * L * k, hipMemcpyHostToDevice, c->stream));
-  launch_gemm_nn(c->stream, A.desc(), L, d, L, Y.desc(), Y.n_local, alpha, beta);
+  {
+    ProfScope ps(c, K_GEMM_NN, 8.0 * Y.n_local * (L + (beta == 0.0 ? 1.0 : 2.0) * k));
+    launch_gemm_nn(c->stream, A.desc(), L, d, L, Y.desc(), Y.n_local, alpha, beta);
+  }
   // the pinned staging buffer is reused by the next call: keep the copy ordered
   MIG_HIP(hipStreamSynchronize(c->stream));
 }
@@ -221,10 +296,12 @@ void mv_add_mv(double alpha, const migmres_mv &A, double beta, const migmres_mv 
   same_rows(A, Y);
   same_rows(B, Y);
   MIG_CHECK(A.ncols == Y.ncols && B.ncols == Y.ncols, "MvAddMv column counts differ");
+  ProfScope ps(Y.ctx, K_AXPBY, 24.0 * Y.n_local * Y.ncols);
   launch_axpby(Y.ctx->stream, alpha, A.desc(), beta, B.desc(), Y.desc(), Y.n_local);
 }
 
 void mv_scale(migmres_mv &Y, double alpha) {
+  ProfScope ps(Y.ctx, K_SCALE, 16.0 * Y.n_local * Y.ncols);
   launch_scale(Y.ctx->stream, Y.desc(), Y.n_local, alpha, nullptr);
 }
 
@@ -257,8 +334,14 @@ void mv_trans_mv(double alpha, const migmres_mv &A, const migmres_mv &B, double 
         views.push_back(Av);
         double *part = c->partial((size_t)nblk * lc * kc);
         double *tmp = c->coef((size_t)lc * kc);
-        launch_gemm_tn_partial(c->stream, Av->desc(), lc, Bv->desc(), kc, A.n_local, part, nblk);
-        launch_reduce_partials(c->stream, part, nblk, lc * kc, alpha, tmp);
+        {
+          ProfScope ps(c, K_GEMM_TN, 8.0 * A.n_local * (lc + kc) + 8.0 * nblk * lc * kc);
+          launch_gemm_tn_partial(c->stream, Av->desc(), lc, Bv->desc(), kc, A.n_local, part, nblk);
+        }
+        {
+          ProfScope ps(c, K_REDUCE, 8.0 * nblk * lc * kc + 8.0 * lc * kc);
+          launch_reduce_partials(c->stream, part, nblk, lc * kc, alpha, tmp);
+        }
         MIG_HIP(hipMemcpy2DAsync(red + a0 + (size_t)b0 * L, sizeof(double) * L, tmp,
                                  sizeof(double) * lc, sizeof(double) * lc, kc,
                                  hipMemcpyDeviceToDevice, c->stream));
@@ -286,7 +369,10 @@ static void coldot_reduce(const migmres_mv &A, const migmres_mv &B, int op, doub
   const int nblk = coldot_blocks(A.n_local);
   double *part = c->partial((size_t)nblk * k);
   double *red = c->red((size_t)k);
-  launch_coldot_partial(c->stream, A.desc(), B.desc(), A.n_local, op, part, nblk);
+  {
+    ProfScope ps(c, K_COLDOT, 8.0 * A.n_local * k * (op == 0 ? 2.0 : 1.0));
+    launch_coldot_partial(c->stream, A.desc(), B.desc(), A.n_local, op, part, nblk);
+  }
   if (op == 2)
     launch_reduce_max(c->stream, part, nblk, k, red);
   else
@@ -315,7 +401,10 @@ void mv_norm(const migmres_mv &A, double *out, int type) {
   }
 }
 
-void mv_init(migmres_mv &Y, double alpha) { launch_fill(Y.ctx->stream, Y.desc(), Y.n_local, alpha); }
+void mv_init(migmres_mv &Y, double alpha) {
+  ProfScope ps(Y.ctx, K_FILL, 8.0 * Y.n_local * Y.ncols);
+  launch_fill(Y.ctx->stream, Y.desc(), Y.n_local, alpha);
+}
 
 void mv_random(migmres_mv &Y, unsigned int *seed) {
   migmres_ctx *c = Y.ctx;
@@ -349,6 +438,7 @@ void mv_random(migmres_mv &Y, unsigned int *seed) {
 void mv_assign(const migmres_mv &A, migmres_mv &Y) {
   same_rows(A, Y);
   MIG_CHECK(A.ncols == Y.ncols, "Assign column counts differ");
+  ProfScope ps(Y.ctx, K_COPY, 16.0 * Y.n_local * Y.ncols);
   launch_copy(Y.ctx->stream, A.desc(), Y.desc(), Y.n_local);
 }
 
@@ -504,6 +594,7 @@ void crs_apply(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, double alpha,
     MIG_NCCL(ncclGroupEnd());
     c->comm_seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
+  ProfScope ps(c, K_SPMM, 12.0 * A.nnz + 4.0 * (A.n_local + 1) + 8.0 * A.n_local * k * (beta == 0.0 ? 2.0 : 3.0));
   launch_spmm(c->stream, 0, A.n_local, A.d_rowptr, A.d_cols, A.d_vals, X.desc(), A.n_local,
               A.d_ghost, n_remote, Y.desc(), alpha, beta);
 }

@@ -10,8 +10,37 @@
 #include "internal.h"
 #include "plan.h"
 
+// Per-kernel-class profiling with HIP events on the context stream (bench.py roofline).
+enum KernelClass { K_SPMM = 0, K_GEMM_TN, K_REDUCE, K_GEMM_NN, K_COLDOT, K_AXPBY, K_SCALE, K_FILL,
+                   K_COPY, K_RANDOM, K_PACK, K_NUM_CLASSES };
+extern const char *kKernelClassNames[K_NUM_CLASSES];
+
+struct migmres_ctx;
+struct ProfScope {
+  migmres_ctx *c;
+  int cls;
+  double bytes;
+  hipEvent_t a = nullptr, b = nullptr;
+  ProfScope(migmres_ctx *ctx, int cls, double bytes);
+  ~ProfScope();
+};
+
 struct migmres_ctx {
   int device = 0, rank = 0, nranks = 1;
+  // profiling state
+  bool prof_on = false;
+  struct Pending {
+    int cls;
+    double bytes;
+    hipEvent_t a, b;
+  };
+  std::vector<Pending> pending;
+  std::vector<hipEvent_t> event_pool;
+  double prof_ms[K_NUM_CLASSES] = {};
+  double prof_bytes[K_NUM_CLASSES] = {};
+  long long prof_count[K_NUM_CLASSES] = {};
+  hipEvent_t get_event();
+  void prof_collect();
   hipStream_t stream = nullptr;
   ncclComm_t comm = nullptr;
   // device scratch: per-workgroup partials, reduced results, staged coefficients
