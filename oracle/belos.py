@@ -206,6 +206,9 @@ class ICGS:
 # ---------------------------------------------------------------------------
 
 
+LP_AUGMENT_SEED = 20250219  # MvRandom stream for augmented right-hand sides
+
+
 class LinearProblem:
     """BelosLinearProblem for an unpreconditioned operator (BelosLinearProblem.hpp)."""
 
@@ -216,6 +219,7 @@ class LinearProblem:
         self.n_apply = 0
         self.ls_num = 0
         self.ls_idx = []
+        self.aug_seed = LP_AUGMENT_SEED
 
     def apply(self, x):
         self.n_apply += 1
@@ -229,31 +233,46 @@ class LinearProblem:
         return True
 
     def set_ls_index(self, idx):
-        """setLSIndex (BelosLinearProblem.hpp:642-705) for non-augmented blocks."""
+        """setLSIndex (BelosLinearProblem.hpp:642-705).  With -1 entries the block is
+        augmented: curX = zeros, curB = random, valid columns copied in (SetBlock)."""
         self.ls_idx = list(idx)
         self.ls_num += 1
-        self.cur = [i for i in idx if i >= 0]
+        self.vld = [i for i in idx if i >= 0]
+        self.new = [j for j, i in enumerate(idx) if i >= 0]
+        bs = len(idx)
+        if len(self.vld) != bs:
+            self.curX = np.zeros((self.X.shape[0], bs))
+            self.curB, self.aug_seed = epetra.epetra_random_mv(self.aug_seed, self.B.shape[0], bs)
+            self.curB[:, self.new] = self.B[:, self.vld]
+            self.curX[:, self.new] = self.X[:, self.vld]
+        else:
+            self.curX = self.X[:, idx].copy()
+            self.curB = self.B[:, idx].copy()
+
+    def set_curr_ls(self):
+        """setCurrLS (BelosLinearProblem.hpp:709-739): copy the solved columns back."""
+        self.X[:, self.vld] = self.curX[:, self.new]
 
     def cur_x(self):
-        return self.X[:, self.cur]
+        return self.curX
 
     def cur_b(self):
-        return self.B[:, self.cur]
+        return self.curB
 
     def update_solution(self, update, update_lp):
         """updateSolution (BelosLinearProblem.hpp:743-812), no right preconditioner."""
         if update is None:
-            return self.cur_x() if not update_lp else self.cur_x()
+            return self.curX
         if update_lp:
-            self.X[:, self.cur] = self.X[:, self.cur] + update
-            return self.cur_x()
-        return self.cur_x() + update
+            self.curX = self.curX + update
+            return self.curX
+        return self.curX + update
 
     def curr_res_vec(self, Xs=None):
         """computeCurrResVec (BelosLinearProblem.hpp:1196-1231): R = B - A X."""
-        Xs = self.cur_x() if Xs is None else Xs
+        Xs = self.curX if Xs is None else Xs
         R = self.apply(Xs)
-        return (-1.0 * R) + (1.0 * self.cur_b())
+        return (-1.0 * R) + (1.0 * self.curB)
 
 
 class StatusTestMaxIters:
@@ -624,10 +643,11 @@ class BlockGmresSolMgr:
                         converged = False
                     break
             if self.imp.cur_soln is not None:
-                lp.X[:, lp.cur] = self.imp.cur_soln
+                lp.curX = 0.0 * self.imp.cur_soln + 1.0 * self.imp.cur_soln
             else:
                 upd = it.current_update()
                 lp.update_solution(upd, True)
+            lp.set_curr_ls()
             self.n_restarts_total += restarts
             start += cur_rhs
             to_solve -= cur_rhs

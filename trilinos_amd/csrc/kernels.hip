@@ -57,18 +57,33 @@ __global__ __launch_bounds__(256) void k_spmm(int row_begin, int row_end,
     }
   }
   const int e0 = rowptr[r], e1 = rowptr[r + 1];
-  for (int e = e0; e < e1; ++e) {
-    const int col = cols[e];
-    const double v = vals[e];
-    if (col < n_local) {
+  // Entries in batches of 8: every index/value load and x-gather of a batch is issued
+  // before the sums consume them.  An empty slot loads a valid address (the row's first
+  // entry) and adds exactly +0.0, which leaves the stored-order sum unchanged (the sum
+  // starts at +0.0 and can never become -0.0).
+  for (int eb = e0; eb < e1; eb += 8) {
+    int ci[8];
+    double v[8];
 #pragma unroll
-      for (int c = 0; c < KC; ++c)
-        if (c < kc) sum[c] = sum[c] + v * xc[c][col];
-    } else {
+    for (int j = 0; j < 8; ++j) {
+      const int e = (eb + j < e1) ? eb + j : e0;
+      ci[j] = cols[e];
+      v[j] = vals[e];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const bool ok = eb + j < e1;
+      const int col = ci[j];
+      const bool own = col < n_local;
       const int g = col - n_local;
 #pragma unroll
-      for (int c = 0; c < KC; ++c)
-        if (c < kc) sum[c] = sum[c] + v * gc[c][g];
+      for (int c = 0; c < KC; ++c) {
+        if (c < kc) {
+          const double x = own ? xc[c][col] : gc[c][g];
+          const double prod = v[j] * x;
+          sum[c] = sum[c] + (ok ? prod : 0.0);
+        }
+      }
     }
   }
 #pragma unroll
@@ -108,129 +123,167 @@ void launch_spmm(hipStream_t s, int row_begin, int row_end, const int *rowptr, c
 
 // -------------------------------------------------------------------------------------
 // C = A^T B (A: nrows x L, B: nrows x kb <= 16) on v_mfma_f64_16x16x4_f64.
-// MFMA M = 16 columns of A, N = 16 columns of B, K = 4 rows per instruction; the row
-// reduction happens inside the matrix core.  A workgroup streams 64-row tiles: B tile
-// (64x16) and A column groups (64 rows x 64 cols, 8 coalesced dwordx4 loads per thread,
-// each wave-instruction = 2 full 512-B column segments) are staged through LDS; wave w
-// owns column tile w of each 64-column group.  Per-workgroup partials are summed by
-// k_reduce in a fixed order.
+// MFMA M = 16 columns of A (one column tile), N = 16 columns of B, K = rows.
+// The K index of an MFMA may map to ANY row as long as A and B agree, so each lane loads
+// 16 bytes = two consecutive rows of one column straight into the operand layout:
+// for 64-row chunk r0 and pair p (0..7), lane l (c = l&15, g = l>>4) holds rows
+// r0 + 8p + 2g and +1 of column c; MFMA 2p uses the first, MFMA 2p+1 the second.
+// A wave-instruction then reads 16 columns x 64 contiguous bytes, and two consecutive
+// instructions consume whole 128-byte lines -- no LDS, no barriers in the main loop.
+// Waves stream 64-row chunks (grid-stride, grid sized to residency); blockIdx.y selects a
+// group of MAXT column tiles; B's fragment is loaded once per chunk and reused across
+// the tiles; the next tile's A fragment is loaded before the current tile's 16 MFMAs.
+// The four waves' accumulators are summed through LDS, one partial per workgroup.
 // f64 MFMA lane maps: A[i=l&15][k=l>>4], B[k=l>>4][j=l&15], D[row=(l>>4)+4r][col=l&15].
 // -------------------------------------------------------------------------------------
 constexpr int TN_ROWS = 64;
-constexpr int TN_APITCH = 66;  // doubles; 66 = 2 mod 32 -> conflict-free ds_read_b64
 
-template <int MAXG>
+template <int MAXT>
 __global__ __launch_bounds__(256) void k_gemm_tn(MvDesc A, int L, MvDesc B, int kb, int nrows,
                                                  double *__restrict__ partial) {
-  __shared__ __attribute__((aligned(16))) double As[64 * TN_APITCH];
-  __shared__ __attribute__((aligned(16))) double Bs[TN_ROWS * 16];
-  const int t = threadIdx.x, l = t & 63, w = t >> 6;
-  const int ngroups = (L + 63) >> 6;
-  d4 acc[MAXG];
-#pragma unroll
-  for (int g = 0; g < MAXG; ++g) acc[g] = d4{0.0, 0.0, 0.0, 0.0};
+  __shared__ __attribute__((aligned(16))) double red[2][MAXT * 4][64];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int c = l & 15, g = l >> 4;
+  const int ntiles = (L + 15) >> 4;
+  const int t0 = blockIdx.y * MAXT;
+  const int nt = (ntiles - t0) < MAXT ? (ntiles - t0) : MAXT;
+  const long long nchunks = (nrows + TN_ROWS - 1) / TN_ROWS;
+  const long long wid = (long long)blockIdx.x * 4 + w, nw = (long long)gridDim.x * 4;
 
-  for (long long rt = blockIdx.x; rt * TN_ROWS < nrows; rt += gridDim.x) {
-    const long long r0 = rt * TN_ROWS;
+  const double *acol[MAXT];
+#pragma unroll
+  for (int tt = 0; tt < MAXT; ++tt) {
+    const int col = (t0 + tt) * 16 + c;
+    acol[tt] = (tt < nt && col < L) ? colp(A, col) : nullptr;
+  }
+  const double *bcol = c < kb ? colp(B, c) : nullptr;
+
+  d4 acc[MAXT];
+#pragma unroll
+  for (int tt = 0; tt < MAXT; ++tt) acc[tt] = d4{0.0, 0.0, 0.0, 0.0};
+
+  for (long long ch = wid; ch < nchunks; ch += nw) {
+    const long long r0 = ch * TN_ROWS;
     const bool full = r0 + TN_ROWS <= nrows;
-    {  // stage B: thread -> column j = t>>4, rows 4*(t&15) .. +3
-      const int j = t >> 4, rr = (t & 15) * 4;
-      double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
-      if (j < kb) {
-        const double *bp = colp(B, j) + r0 + rr;
-        if (full) {
-          const d2 p = *(const d2 *)bp, q = *(const d2 *)(bp + 2);
-          v0 = p.x; v1 = p.y; v2 = q.x; v3 = q.y;
-        } else {
-          v0 = (r0 + rr + 0 < nrows) ? bp[0] : 0.0;
-          v1 = (r0 + rr + 1 < nrows) ? bp[1] : 0.0;
-          v2 = (r0 + rr + 2 < nrows) ? bp[2] : 0.0;
-          v3 = (r0 + rr + 3 < nrows) ? bp[3] : 0.0;
-        }
-      }
-      Bs[(rr + 0) * 16 + j] = v0;
-      Bs[(rr + 1) * 16 + j] = v1;
-      Bs[(rr + 2) * 16 + j] = v2;
-      Bs[(rr + 3) * 16 + j] = v3;
-    }
+    auto ld2 = [&](const double *p, long long r) -> d2 {
+      if (!p) return d2{0.0, 0.0};
+      if (full) return *(const d2 *)(p + r);
+      return d2{r < nrows ? p[r] : 0.0, r + 1 < nrows ? p[r + 1] : 0.0};
+    };
+    d2 bq[8];
 #pragma unroll
-    for (int g = 0; g < MAXG; ++g) {
-      if (g < ngroups) {
-        d2 v[8];
+    for (int p = 0; p < 8; ++p) bq[p] = ld2(bcol, r0 + 8 * p + 2 * g);
+    d2 cur[8], nxt[8];
 #pragma unroll
-        for (int s = 0; s < 8; ++s) {
-          const int cl = 8 * s + (t >> 5);
-          const int cg = g * 64 + cl;
-          const int rr = 2 * (t & 31);
-          v[s] = d2{0.0, 0.0};
-          if (cg < L) {
-            const double *ap = colp(A, cg) + r0 + rr;
-            if (full) {
-              v[s] = *(const d2 *)ap;
-            } else {
-              v[s].x = (r0 + rr < nrows) ? ap[0] : 0.0;
-              v[s].y = (r0 + rr + 1 < nrows) ? ap[1] : 0.0;
-            }
-          }
+    for (int p = 0; p < 8; ++p) cur[p] = ld2(acol[0], r0 + 8 * p + 2 * g);
+#pragma unroll
+    for (int tt = 0; tt < MAXT; ++tt) {
+      if (tt < nt) {
+        if (tt + 1 < nt) {
+#pragma unroll
+          for (int p = 0; p < 8; ++p) nxt[p] = ld2(acol[tt + 1], r0 + 8 * p + 2 * g);
         }
 #pragma unroll
-        for (int s = 0; s < 8; ++s) {
-          const int cl = 8 * s + (t >> 5);
-          *(d2 *)&As[cl * TN_APITCH + 2 * (t & 31)] = v[s];
+        for (int p = 0; p < 8; ++p) {
+          acc[tt] = __builtin_amdgcn_mfma_f64_16x16x4f64(cur[p].x, bq[p].x, acc[tt], 0, 0, 0);
+          acc[tt] = __builtin_amdgcn_mfma_f64_16x16x4f64(cur[p].y, bq[p].y, acc[tt], 0, 0, 0);
         }
-        __syncthreads();
-        if (g * 64 + 16 * w < L) {
+        if (tt + 1 < nt) {
 #pragma unroll
-          for (int q = 0; q < TN_ROWS / 4; ++q) {
-            const double a = As[(16 * w + (l & 15)) * TN_APITCH + 4 * q + (l >> 4)];
-            const double b = Bs[(4 * q + (l >> 4)) * 16 + (l & 15)];
-            acc[g] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[g], 0, 0, 0);
-          }
+          for (int p = 0; p < 8; ++p) cur[p] = nxt[p];
         }
-        __syncthreads();
       }
     }
   }
-  double *out = partial + (long long)blockIdx.x * L * kb;
-  const int j = l & 15;
+  // sum the four waves' accumulators: (2,3) -> (0,1) -> 0
+  if (w >= 2) {
 #pragma unroll
-  for (int g = 0; g < MAXG; ++g) {
-    if (g < ngroups && g * 64 + 16 * w < L && j < kb) {
+    for (int tt = 0; tt < MAXT; ++tt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = g * 64 + 16 * w + (l >> 4) + 4 * r;
-        if (i < L) out[i + (long long)j * L] = acc[g][r];
+      for (int r = 0; r < 4; ++r) red[w - 2][tt * 4 + r][l] = acc[tt][r];
+  }
+  __syncthreads();
+  if (w < 2) {
+#pragma unroll
+    for (int tt = 0; tt < MAXT; ++tt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[tt][r] += red[w][tt * 4 + r][l];
+  }
+  __syncthreads();
+  if (w == 1) {
+#pragma unroll
+    for (int tt = 0; tt < MAXT; ++tt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[0][tt * 4 + r][l] = acc[tt][r];
+  }
+  __syncthreads();
+  if (w == 0 && c < kb) {
+    double *out = partial + (long long)blockIdx.x * L * kb;
+#pragma unroll
+    for (int tt = 0; tt < MAXT; ++tt) {
+      if (tt < nt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = (t0 + tt) * 16 + g + 4 * r;
+          if (i < L) out[i + (long long)c * L] = acc[tt][r] + red[0][tt * 4 + r][l];
+        }
       }
     }
   }
 }
 
+constexpr int TN_MAXT = 8;
+
+static int tn_resident_blocks() {
+  static int cached = 0;
+  if (!cached) {
+    int per_cu = 0, dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_gemm_tn<TN_MAXT>, 256, 0) != hipSuccess ||
+        per_cu < 1 || cus < 1)
+      return 512;
+    cached = per_cu * cus;
+  }
+  return cached;
+}
+
 int gemm_tn_blocks(int nrows) {
-  const int tiles = cdiv(nrows, TN_ROWS);
-  return tiles < 1024 ? (tiles > 0 ? tiles : 1) : 1024;
+  const long long waves = (nrows + TN_ROWS - 1) / TN_ROWS;
+  long long b = (waves + 3) / 4;
+  const int cap = tn_resident_blocks();
+  if (b > cap) b = cap;
+  return b < 1 ? 1 : (int)b;
 }
 
 void launch_gemm_tn_partial(hipStream_t s, MvDesc A, int L, MvDesc B, int kb, int nrows,
                             double *partial, int nblocks) {
   if (L > 512 || kb > 16) throw Error(MIGMRES_EINVAL, "gemm_tn: L <= 512 and kb <= 16 per launch");
-  if (L <= 128)
-    k_gemm_tn<2><<<nblocks, 256, 0, s>>>(A, L, B, kb, nrows, partial);
-  else if (L <= 256)
-    k_gemm_tn<4><<<nblocks, 256, 0, s>>>(A, L, B, kb, nrows, partial);
-  else
-    k_gemm_tn<8><<<nblocks, 256, 0, s>>>(A, L, B, kb, nrows, partial);
+  const int ntiles = (L + 15) / 16;
+  const dim3 grid(nblocks, (ntiles + TN_MAXT - 1) / TN_MAXT);
+  k_gemm_tn<TN_MAXT><<<grid, 256, 0, s>>>(A, L, B, kb, nrows, partial);
   LAUNCH_CHECK();
 }
 
 __global__ __launch_bounds__(256) void k_reduce(const double *__restrict__ partial, int nblocks,
                                                 int nout, double alpha, double *__restrict__ out) {
+  // 64 outputs x 4 slices per workgroup; each thread keeps 4 independent running sums
+  // over blocks b = s, s+4, ... so loads stay in flight; fixed combine order.
   __shared__ double red[4][64];
   const int l = threadIdx.x & 63, s = threadIdx.x >> 6;
   const int o = blockIdx.x * 64 + l;
-  double acc = 0.0;
-  if (o < nout)
-    for (int b = s; b < nblocks; b += 4) acc += partial[(long long)b * nout + o];
-  red[s][l] = acc;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  if (o < nout) {
+    int b = s;
+    for (; b + 12 < nblocks; b += 16) {
+      a0 += partial[(long long)b * nout + o];
+      a1 += partial[(long long)(b + 4) * nout + o];
+      a2 += partial[(long long)(b + 8) * nout + o];
+      a3 += partial[(long long)(b + 12) * nout + o];
+    }
+    for (; b < nblocks; b += 4) a0 += partial[(long long)b * nout + o];
+  }
+  red[s][l] = (a0 + a1) + (a2 + a3);
   __syncthreads();
   if (s == 0 && o < nout) out[o] = alpha * ((red[0][l] + red[1][l]) + (red[2][l] + red[3][l]));
 }

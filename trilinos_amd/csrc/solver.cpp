@@ -323,14 +323,50 @@ struct Problem {  // LinearProblem without preconditioners
     apply(*X, *R0);
     mv_add_mv(-1.0, *R0, 1.0, *B, *R0);
   }
-  void set_ls_index(const std::vector<int> &idx) {  // setLSIndex
+  unsigned int aug_seed = 20250219u;  // MvRandom stream for augmented right-hand sides
+  std::vector<int> vld, newi;
+  bool augmented = false;
+
+  // setLSIndex (BelosLinearProblem.hpp:642-705): a block with -1 entries is augmented --
+  // curX = zeros and curB = random with the valid columns copied in (SetBlock).
+  void set_ls_index(const std::vector<int> &idx) {
     ls_idx = idx;
     ++ls_num;
     cur.clear();
-    for (int i : idx)
-      if (i >= 0) cur.push_back(i);
-    curX = MvPtr(mv_view(X, cur.data(), (int)cur.size()));
-    curB = MvPtr(mv_view(B, cur.data(), (int)cur.size()));
+    vld.clear();
+    newi.clear();
+    for (size_t j = 0; j < idx.size(); ++j)
+      if (idx[j] >= 0) {
+        cur.push_back(idx[j]);
+        vld.push_back(idx[j]);
+        newi.push_back((int)j);
+      }
+    const int bs = (int)idx.size();
+    augmented = (int)vld.size() != bs;
+    if (augmented) {
+      curX = MvPtr(mv_create(X->ctx, X->n_global, X->n_local, bs));
+      mv_init(*curX, 0.0);
+      curB = MvPtr(mv_create(B->ctx, B->n_global, B->n_local, bs));
+      mv_random(*curB, &aug_seed);
+      MvPtr bsrc(mv_view(B, vld.data(), (int)vld.size()));
+      MvPtr bdst(mv_view(curB.p, newi.data(), (int)newi.size()));
+      mv_assign(*bsrc, *bdst);
+      MvPtr xsrc(mv_view(X, vld.data(), (int)vld.size()));
+      MvPtr xdst(mv_view(curX.p, newi.data(), (int)newi.size()));
+      mv_assign(*xsrc, *xdst);
+      MIG_HIP(hipStreamSynchronize(X->ctx->stream));
+    } else {
+      curX = MvPtr(mv_view(X, cur.data(), (int)cur.size()));
+      curB = MvPtr(mv_view(B, cur.data(), (int)cur.size()));
+    }
+  }
+  // setCurrLS (BelosLinearProblem.hpp:709-739)
+  void set_curr_ls() {
+    if (!augmented) return;
+    MvPtr src(mv_view(curX.p, newi.data(), (int)newi.size()));
+    MvPtr dst(mv_view(X, vld.data(), (int)vld.size()));
+    mv_assign(*src, *dst);
+    MIG_HIP(hipStreamSynchronize(X->ctx->stream));
   }
   // computeCurrResVec: R = B - A*Xs (BelosLinearProblem.hpp:1196-1231)
   void curr_res_vec(migmres_mv &R, const migmres_mv *Xs = nullptr) {
@@ -701,11 +737,12 @@ struct Engine {
         }
       }
       if (imp.have_soln) {
-        mv_assign(*imp.cur_soln, *lp.curX);
+        mv_add_mv(0.0, *imp.cur_soln, 1.0, *imp.cur_soln, *lp.curX);
       } else {
         MvPtr upd = current_update(it);
         if (upd.p) mv_add_mv(1.0, *lp.curX, 1.0, *upd, *lp.curX);
       }
+      lp.set_curr_ls();
       S->n_restarts += restarts;
       start += cur_rhs;
       to_solve -= cur_rhs;
