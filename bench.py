@@ -142,7 +142,7 @@ def main():
         import ctypes as C
         call("migmres_ctx_profile", comm.h, 1)
         run(args.steps)
-        nk = 11
+        nk = 12
         ms, by, cnt = (C.c_double * nk)(), (C.c_double * nk)(), (C.c_longlong * nk)()
         call("migmres_ctx_profile_read", comm.h, ms, by, cnt, nk)
         call("migmres_ctx_profile", comm.h, 0)

@@ -188,7 +188,8 @@ int migmres_solver_history(const migmres_solver *s, double *out, int *nrows, int
  * [3] blkOrthoSing fallbacks, [4] block iterations. */
 int migmres_solver_counters(const migmres_solver *s, long long *out, int n);
 /* Seconds spent in named phases: [0] total solve, [1] SpMM, [2] orthogonalization,
- * [3] host least-squares, [4] communication. */
+ * [3] host least-squares, [4] communication, [5] status tests, [6] restarts, [7] setup.
+ * With "Verbosity" bit 1 set the phases are separated by stream synchronisations. */
 int migmres_solver_timers(const migmres_solver *s, double *out, int n);
 
 #ifdef __cplusplus

@@ -293,9 +293,9 @@ class BlockGmresSolMgr:
         return dict(zip(keys, list(out)))
 
     def timers(self):
-        out = (C.c_double * 5)()
-        call("migmres_solver_timers", self.h, out, 5)
-        keys = ("total", "spmm", "ortho", "lsqr", "comm")
+        out = (C.c_double * 8)()
+        call("migmres_solver_timers", self.h, out, 8)
+        keys = ("total", "spmm", "ortho", "lsqr", "comm", "status", "restart", "setup")
         return dict(zip(keys, list(out)))
 
     def __del__(self):

@@ -1,0 +1,35 @@
+// Device-resident ICGS state and kernel launchers (icgs.hip).
+#pragma once
+
+#include "internal.h"
+
+namespace migmres {
+
+// Coefficients and decisions of one projectAndNormalize / normalize call, kept on the
+// device between kernels and copied to the host once at the end.
+struct IcgsState {
+  double oldDot[16], newDot[16], diag[16], inv[16], P[16], P2[16], prod[16];
+  double B[256];  // k x k normalisation coefficients, column-major, leading dimension 16
+  double blk_old[16];
+  double blk_tol, sing_tol, dep, neg;
+  int failed;  // first findBasis column found dependent, -1 if none
+  int pad_;
+};
+
+int icgs_blocks(int nrows);
+void launch_reduce_small(hipStream_t s, const double *partial, int nblocks, int nv, double *out);
+void launch_gemm_nn_dot(hipStream_t s, MvDesc A, int L, const double *M, int ldm, MvDesc X,
+                        int nrows, double alpha, double beta, int dmode, MvDesc D, double *partial,
+                        int nblocks);
+void launch_fb_a(hipStream_t s, MvDesc X, int j, const IcgsState *st, int nrows, double *partial, int nb);
+void launch_fb_b(hipStream_t s, MvDesc X, int j, const IcgsState *st, double *S, int nrows, double *partial, int nb);
+void launch_fb_c(hipStream_t s, MvDesc X, int j, const IcgsState *st, const double *S, int nrows, double *partial,
+                 int nb);
+void launch_scale_col(hipStream_t s, MvDesc X, int j, const IcgsState *st, int nrows);
+void launch_fb_scalar(hipStream_t s, IcgsState *st, const double *red, int stage, int j, int k, int complete);
+void launch_blk_old(hipStream_t s, IcgsState *st, const double *G, int ldg, int L, int k);
+void launch_state_reset(hipStream_t s, IcgsState *st, double blk_tol, double sing_tol);
+void launch_add_coef(hipStream_t s, const double *C1, int ld1, const double *C2, int ld2, double *out, int ldo,
+                     int L, int k);
+
+}  // namespace migmres

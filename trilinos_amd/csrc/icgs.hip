@@ -1,0 +1,406 @@
+// Device-resident ICGS building blocks (belos/src/BelosICGSOrthoManager.hpp).
+//
+// The reference drives ICGS from the host: every inner product is a MvTransMv/MvDot whose
+// result comes back to the host before the next update.  Here the coefficients stay in a
+// device state block (IcgsState) and every step reads what the previous step reduced, so a
+// whole projectAndNormalize is one stream of kernels with a single device-to-host copy at
+// the end.  Decisions the reference takes between steps (dependency tests, rank) are
+// recorded as flags and acted on by the host afterwards (the fallback restarts from the
+// saved input block, exactly as the reference restarts from tmpX).
+//
+//   k_gemm_nn_dot   X = beta X + alpha A M, plus per-column partials of sum(X_new * D)
+//                   (blkOrtho's second update fused with MvDot(X, X), newDot)
+//   k_fb_a/b/c      findBasis column j (BelosICGSOrthoManager.hpp:1002-1091): oldDot and
+//                   the first projection; first update fused with the second projection;
+//                   second update fused with newDot = <Xj, oldMXj>
+//   k_fb_scalar     the scalar logic between those steps (diag, dependency flags, B column)
+#include "icgs.h"
+
+namespace migmres {
+
+typedef double d2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ double *colp_(const MvDesc &d, int c) {
+  return d.base + (long long)(d.cols ? d.cols[c] : c) * d.ld;
+}
+static inline int cdiv_(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+#define LAUNCH_CHECK_()                                                                     \
+  do {                                                                                      \
+    hipError_t e_ = hipGetLastError();                                                      \
+    if (e_ != hipSuccess) throw Error(MIGMRES_EHIP, std::string("kernel launch: ") + hipGetErrorString(e_)); \
+  } while (0)
+
+// Fixed-order block reduction of NV values per thread -> partial[blockIdx.x * NV + i].
+template <int NV>
+__device__ __forceinline__ void block_reduce_store(double (&v)[NV], int nv, double *partial) {
+  __shared__ double red[4][NV];
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    if (i < nv) {
+      double x = v[i];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off, 64);
+      if (l == 0) red[w][i] = x;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < nv) {
+    const int i = threadIdx.x;
+    partial[(long long)blockIdx.x * nv + i] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
+  }
+}
+
+int icgs_blocks(int nrows) {
+  const int b = cdiv_(nrows, 4096);
+  return b < 1 ? 1 : (b > 512 ? 512 : b);
+}
+
+// out[o] = sum_b partial[b * nv + o], o < nv <= 17: one workgroup, every thread sums a
+// fixed subset of blocks for all outputs, then a fixed-shape tree (deterministic).
+__global__ __launch_bounds__(256) void k_reduce_small(const double *__restrict__ partial, int nblocks,
+                                                      int nv, double *__restrict__ out) {
+  double v[17];
+#pragma unroll
+  for (int i = 0; i < 17; ++i) v[i] = 0.0;
+  for (int b = threadIdx.x; b < nblocks; b += 256) {
+#pragma unroll
+    for (int i = 0; i < 17; ++i)
+      if (i < nv) v[i] += partial[(long long)b * nv + i];
+  }
+  __shared__ double red[4][17];
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < 17; ++i) {
+    if (i < nv) {
+      double x = v[i];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off, 64);
+      if (l == 0) red[w][i] = x;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < nv) {
+    const int i = threadIdx.x;
+    out[i] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
+  }
+}
+
+void launch_reduce_small(hipStream_t s, const double *partial, int nblocks, int nv, double *out) {
+  k_reduce_small<<<1, 256, 0, s>>>(partial, nblocks, nv, out);
+  LAUNCH_CHECK_();
+}
+
+// -------------------------------------------------------------------------------------
+// X = beta X + alpha A M (M device, L x kx, leading dim ldm) and, if dmode != 0, partials
+// of sum_r Xnew[r,c] * D[r,c] (dmode 1: D = Xnew, 2: D given).  Grid-stride over row pairs.
+// -------------------------------------------------------------------------------------
+template <int KX>
+__global__ __launch_bounds__(256) void k_gemm_nn_dot(MvDesc A, int L, const double *__restrict__ M,
+                                                     int ldm, MvDesc X, int kx, int nrows,
+                                                     double alpha, double beta, int dmode,
+                                                     MvDesc D, double *__restrict__ partial) {
+  extern __shared__ __attribute__((aligned(16))) double Ms[];  // L x KX
+  for (int e = threadIdx.x; e < L * KX; e += 256) {
+    const int j = e / KX, c = e % KX;
+    Ms[e] = c < kx ? M[j + (long long)c * ldm] : 0.0;
+  }
+  __syncthreads();
+  double dacc[KX];
+#pragma unroll
+  for (int c = 0; c < KX; ++c) dacc[c] = 0.0;
+  for (long long r = 2LL * ((long long)blockIdx.x * 256 + threadIdx.x); r < nrows;
+       r += 2LL * gridDim.x * 256) {
+    const bool two = r + 1 < nrows;
+    double acc0[KX], acc1[KX];
+#pragma unroll
+    for (int c = 0; c < KX; ++c) acc0[c] = acc1[c] = 0.0;
+#pragma unroll 4
+    for (int j = 0; j < L; ++j) {
+      const double *ap = colp_(A, j) + r;
+      double a0, a1;
+      if (two) {
+        const d2 v = *(const d2 *)ap;
+        a0 = v.x;
+        a1 = v.y;
+      } else {
+        a0 = ap[0];
+        a1 = 0.0;
+      }
+      const double *mrow = &Ms[j * KX];
+#pragma unroll
+      for (int c = 0; c < KX; ++c) {
+        acc0[c] += a0 * mrow[c];
+        acc1[c] += a1 * mrow[c];
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < KX; ++c) {
+      if (c < kx) {
+        double *xp = colp_(X, c) + r;
+        double n0, n1 = 0.0;
+        if (beta == 0.0) {
+          n0 = alpha * acc0[c];
+          if (two) n1 = alpha * acc1[c];
+        } else {
+          n0 = beta * xp[0] + alpha * acc0[c];
+          if (two) n1 = beta * xp[1] + alpha * acc1[c];
+        }
+        xp[0] = n0;
+        if (two) xp[1] = n1;
+        if (dmode == 1) {
+          dacc[c] += n0 * n0 + n1 * n1;
+        } else if (dmode == 2) {
+          const double *dp = colp_(D, c) + r;
+          dacc[c] += n0 * dp[0] + (two ? n1 * dp[1] : 0.0);
+        }
+      }
+    }
+  }
+  if (dmode) block_reduce_store<KX>(dacc, kx, partial);
+}
+
+void launch_gemm_nn_dot(hipStream_t s, MvDesc A, int L, const double *M, int ldm, MvDesc X,
+                        int nrows, double alpha, double beta, int dmode, MvDesc D, double *partial,
+                        int nblocks) {
+  const int kx = X.ncols;
+  if (kx > 16) throw Error(MIGMRES_EINVAL, "gemm_nn_dot: at most 16 columns");
+  if (L > 1024) throw Error(MIGMRES_EINVAL, "gemm_nn_dot: at most 1024 coefficient rows");
+  const int KX = kx <= 1 ? 1 : kx <= 2 ? 2 : kx <= 4 ? 4 : kx <= 8 ? 8 : 16;
+  const size_t lds = sizeof(double) * (size_t)(L > 0 ? L : 1) * KX;
+  switch (KX) {
+    case 1: k_gemm_nn_dot<1><<<nblocks, 256, lds, s>>>(A, L, M, ldm, X, kx, nrows, alpha, beta, dmode, D, partial); break;
+    case 2: k_gemm_nn_dot<2><<<nblocks, 256, lds, s>>>(A, L, M, ldm, X, kx, nrows, alpha, beta, dmode, D, partial); break;
+    case 4: k_gemm_nn_dot<4><<<nblocks, 256, lds, s>>>(A, L, M, ldm, X, kx, nrows, alpha, beta, dmode, D, partial); break;
+    case 8: k_gemm_nn_dot<8><<<nblocks, 256, lds, s>>>(A, L, M, ldm, X, kx, nrows, alpha, beta, dmode, D, partial); break;
+    default: k_gemm_nn_dot<16><<<nblocks, 256, lds, s>>>(A, L, M, ldm, X, kx, nrows, alpha, beta, dmode, D, partial); break;
+  }
+  LAUNCH_CHECK_();
+}
+
+// -------------------------------------------------------------------------------------
+// findBasis column kernels on the block X (nrows x k, k <= 16), column j.
+// -------------------------------------------------------------------------------------
+// Row pairs: each thread handles rows (r, r+1) with 16-byte loads; the padding row of a
+// pair (r+1 == nrows) reads the zero padding and is never written.
+// (a) normalise column j-1 in place by inv[j-1]; partials [oldDot_j, <X_i, X_j> i<j]
+__global__ __launch_bounds__(256) void k_fb_a(MvDesc X, int j, const IcgsState *__restrict__ st,
+                                              int nrows, double *__restrict__ partial) {
+  double v[17];
+#pragma unroll
+  for (int i = 0; i < 17; ++i) v[i] = 0.0;
+  const double invp = j > 0 ? st->inv[j - 1] : 1.0;
+  double *xj = colp_(X, j);
+  double *xp = j > 0 ? colp_(X, j - 1) : xj;
+  for (long long r = 2LL * ((long long)blockIdx.x * 256 + threadIdx.x); r < nrows;
+       r += 2LL * gridDim.x * 256) {
+    const d2 x = *(const d2 *)(xj + r);
+    v[0] += x.x * x.x + x.y * x.y;
+    if (j > 0) {
+      const d2 p = *(const d2 *)(xp + r);
+      const double q0 = invp * p.x, q1 = invp * p.y;
+      xp[r] = q0;
+      if (r + 1 < nrows) xp[r + 1] = q1;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        if (i < j - 1) {
+          const d2 y = *(const d2 *)(colp_(X, i) + r);
+          v[1 + i] += y.x * x.x + y.y * x.y;
+        } else if (i == j - 1) {
+          v[1 + i] += q0 * x.x + q1 * x.y;
+        }
+      }
+    }
+  }
+  block_reduce_store<17>(v, j + 1, partial);
+}
+
+// (b) x1 = X_j - sum_i X_i P_i  -> S ; partials <X_i, x1> (i < j)
+__global__ __launch_bounds__(256) void k_fb_b(MvDesc X, int j, const IcgsState *__restrict__ st,
+                                              double *__restrict__ S, int nrows,
+                                              double *__restrict__ partial) {
+  double v[16];
+  double P[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    v[i] = 0.0;
+    P[i] = i < j ? st->P[i] : 0.0;
+  }
+  const double *xj = colp_(X, j);
+  for (long long r = 2LL * ((long long)blockIdx.x * 256 + threadIdx.x); r < nrows;
+       r += 2LL * gridDim.x * 256) {
+    d2 q[16];
+    double t0 = 0.0, t1 = 0.0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (i < j) {
+        q[i] = *(const d2 *)(colp_(X, i) + r);
+        t0 += q[i].x * P[i];
+        t1 += q[i].y * P[i];
+      }
+    const d2 x = *(const d2 *)(xj + r);
+    const double a0 = x.x - t0, a1 = x.y - t1;
+    S[r] = a0;
+    if (r + 1 < nrows) S[r + 1] = a1;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (i < j) v[i] += q[i].x * a0 + q[i].y * a1;
+  }
+  block_reduce_store<16>(v, j, partial);
+}
+
+// (c) x2 = S - sum_i X_i P2_i -> X_j ; partials <x2, X_j(old)>
+__global__ __launch_bounds__(256) void k_fb_c(MvDesc X, int j, const IcgsState *__restrict__ st,
+                                              const double *__restrict__ S, int nrows,
+                                              double *__restrict__ partial) {
+  double v[1] = {0.0};
+  double P[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) P[i] = i < j ? st->P2[i] : 0.0;
+  double *xj = colp_(X, j);
+  for (long long r = 2LL * ((long long)blockIdx.x * 256 + threadIdx.x); r < nrows;
+       r += 2LL * gridDim.x * 256) {
+    double t0 = 0.0, t1 = 0.0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (i < j) {
+        const d2 y = *(const d2 *)(colp_(X, i) + r);
+        t0 += y.x * P[i];
+        t1 += y.y * P[i];
+      }
+    const d2 sv = *(const d2 *)(S + r);
+    const d2 old = *(const d2 *)(xj + r);
+    const double a0 = sv.x - t0, a1 = sv.y - t1;
+    v[0] += a0 * old.x + a1 * old.y;
+    xj[r] = a0;
+    if (r + 1 < nrows) xj[r + 1] = a1;
+  }
+  block_reduce_store<1>(v, 1, partial);
+}
+
+__global__ __launch_bounds__(256) void k_scale_col(MvDesc X, int j, const IcgsState *__restrict__ st, int nrows) {
+  const long long r = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (r < nrows) {
+    double *p = colp_(X, j) + r;
+    *p = st->inv[j] * (*p);
+  }
+}
+
+// Scalar step after a reduction (red = reduced vector).  stage: 0 after (a), 1 after (b),
+// 2 after (c), 3 after blkOrtho's projections (C = C1 + C2, dependency test), 4 for the
+// k == 1 normalisation.
+__global__ void k_fb_scalar(IcgsState *st, const double *__restrict__ red, int stage, int j, int k,
+                            int complete) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  if (stage == 0) {
+    st->oldDot[j] = red[0];
+    if (st->oldDot[j] < 0.0) st->neg = 1.0;
+    for (int i = 0; i < j; ++i) {
+      st->P[i] = red[1 + i];
+      st->prod[i] = red[1 + i];
+    }
+    if (j == 0) {  // no projection: newDot = oldDot
+      const double nd = st->oldDot[0];
+      st->newDot[0] = nd;
+      const double tol = complete ? st->sing_tol : st->blk_tol;
+      const bool dep = complete ? fabs(nd) < fabs(tol * st->oldDot[0]) : fabs(nd) < fabs(st->oldDot[0] * tol);
+      if (dep && st->failed < 0) st->failed = 0;
+      const double diag = sqrt(fabs(nd));
+      st->diag[0] = diag;
+      st->inv[0] = 1.0 / diag;
+      st->B[0] = diag;
+    }
+  } else if (stage == 1) {
+    for (int i = 0; i < j; ++i) {
+      st->P2[i] = red[i];
+      st->prod[i] = st->prod[i] + red[i];
+    }
+  } else if (stage == 2) {
+    const double nd = red[0];
+    st->newDot[j] = nd;
+    const double tol = complete ? st->sing_tol : st->blk_tol;
+    const bool dep = complete ? fabs(nd) < fabs(tol * st->oldDot[j]) : fabs(nd) < fabs(st->oldDot[j] * tol);
+    if (dep && st->failed < 0) st->failed = j;
+    const double diag = sqrt(fabs(nd));
+    st->diag[j] = diag;
+    st->inv[j] = 1.0 / diag;
+    st->B[j + 16 * j] = diag;
+    for (int i = 0; i < j; ++i) st->B[i + 16 * j] = st->prod[i];
+  } else if (stage == 3) {
+    // red = newDot (k values); oldDot from the Gram block recorded earlier
+    for (int c = 0; c < k; ++c)
+      if (fabs(red[c]) < fabs(st->blk_old[c] * st->blk_tol)) st->dep = 1.0;
+  } else if (stage == 4) {
+    const double d = red[0];
+    const double b = sqrt(fabs(d));
+    st->B[0] = b;
+    st->diag[0] = b;
+    st->inv[0] = fabs(b) > 0.0 ? 1.0 / b : 1.0;
+  }
+}
+
+// Record blkOrtho's oldDot = diag(X^T X) from the Gram block (rows L..L+k-1 of the
+// (L+k) x k product) and reset the per-call flags.
+__global__ void k_blk_old(IcgsState *st, const double *__restrict__ G, int ldg, int L, int k) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  for (int c = 0; c < k; ++c) st->blk_old[c] = G[(L + c) + (long long)c * ldg];
+}
+
+__global__ void k_state_reset(IcgsState *st, double blk_tol, double sing_tol) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  st->failed = -1;
+  st->dep = 0.0;
+  st->neg = 0.0;
+  st->blk_tol = blk_tol;
+  st->sing_tol = sing_tol;
+  for (int i = 0; i < 256; ++i) st->B[i] = 0.0;
+}
+
+// C_out[i + j*ldo] = C1[i + j*ld1] + C2[i + j*ld2] for i < L, j < k
+__global__ void k_add_coef(const double *__restrict__ C1, int ld1, const double *__restrict__ C2, int ld2,
+                           double *__restrict__ out, int ldo, int L, int k) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= L * k) return;
+  const int i = e % L, j = e / L;
+  out[i + (long long)j * ldo] = C1[i + (long long)j * ld1] + C2[i + (long long)j * ld2];
+}
+
+void launch_fb_a(hipStream_t s, MvDesc X, int j, const IcgsState *st, int nrows, double *partial, int nb) {
+  k_fb_a<<<nb, 256, 0, s>>>(X, j, st, nrows, partial);
+  LAUNCH_CHECK_();
+}
+void launch_fb_b(hipStream_t s, MvDesc X, int j, const IcgsState *st, double *S, int nrows, double *partial, int nb) {
+  k_fb_b<<<nb, 256, 0, s>>>(X, j, st, S, nrows, partial);
+  LAUNCH_CHECK_();
+}
+void launch_fb_c(hipStream_t s, MvDesc X, int j, const IcgsState *st, const double *S, int nrows, double *partial,
+                 int nb) {
+  k_fb_c<<<nb, 256, 0, s>>>(X, j, st, S, nrows, partial);
+  LAUNCH_CHECK_();
+}
+void launch_scale_col(hipStream_t s, MvDesc X, int j, const IcgsState *st, int nrows) {
+  if (nrows <= 0) return;
+  k_scale_col<<<cdiv_(nrows, 256), 256, 0, s>>>(X, j, st, nrows);
+  LAUNCH_CHECK_();
+}
+void launch_fb_scalar(hipStream_t s, IcgsState *st, const double *red, int stage, int j, int k, int complete) {
+  k_fb_scalar<<<1, 64, 0, s>>>(st, red, stage, j, k, complete);
+  LAUNCH_CHECK_();
+}
+void launch_blk_old(hipStream_t s, IcgsState *st, const double *G, int ldg, int L, int k) {
+  k_blk_old<<<1, 64, 0, s>>>(st, G, ldg, L, k);
+  LAUNCH_CHECK_();
+}
+void launch_state_reset(hipStream_t s, IcgsState *st, double blk_tol, double sing_tol) {
+  k_state_reset<<<1, 64, 0, s>>>(st, blk_tol, sing_tol);
+  LAUNCH_CHECK_();
+}
+void launch_add_coef(hipStream_t s, const double *C1, int ld1, const double *C2, int ld2, double *out, int ldo,
+                     int L, int k) {
+  if (L * k <= 0) return;
+  k_add_coef<<<cdiv_((long long)L * k, 256), 256, 0, s>>>(C1, ld1, C2, ld2, out, ldo, L, k);
+  LAUNCH_CHECK_();
+}
+
+}  // namespace migmres

@@ -79,6 +79,10 @@ void launch_gemm_tn_partial(hipStream_t s, MvDesc A, int L, MvDesc B, int kb, in
 void launch_reduce_partials(hipStream_t s, const double *partial, int nblocks, int nout,
                             double alpha, double *out);
 
+// The same with the (rows x cols) result written column-major with leading dimension ldo.
+void launch_reduce_partials_ld(hipStream_t s, const double *partial, int nblocks, int rows, int cols,
+                               int ldo, double alpha, double *out);
+
 // X = beta*X + alpha * A * M, M (L x kx) device column-major with leading dim ldm.
 void launch_gemm_nn(hipStream_t s, MvDesc A, int L, const double *M, int ldm, MvDesc X,
                     int nrows, double alpha, double beta);

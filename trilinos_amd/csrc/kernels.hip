@@ -141,6 +141,10 @@ constexpr int TN_ROWS = 64;
 template <int MAXT>
 __global__ __launch_bounds__(256) void k_gemm_tn(MvDesc A, int L, MvDesc B, int kb, int nrows,
                                                  double *__restrict__ partial) {
+  // Branch-free main loop: every multivector keeps its padding rows [nrows, ld) at zero
+  // (mv_create clears the allocation; kernels only write rows < nrows), so whole 64-row
+  // chunks are read without row guards; columns past L / kb are clamped to a valid column,
+  // and their values only reach output rows >= L / columns >= kb, which are not stored.
   __shared__ __attribute__((aligned(16))) double red[2][MAXT * 4][64];
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int c = l & 15, g = l >> 4;
@@ -153,10 +157,11 @@ __global__ __launch_bounds__(256) void k_gemm_tn(MvDesc A, int L, MvDesc B, int 
   const double *acol[MAXT];
 #pragma unroll
   for (int tt = 0; tt < MAXT; ++tt) {
-    const int col = (t0 + tt) * 16 + c;
-    acol[tt] = (tt < nt && col < L) ? colp(A, col) : nullptr;
+    int col = (t0 + tt) * 16 + c;
+    col = col < L ? col : L - 1;
+    acol[tt] = colp(A, col) + 2 * g;
   }
-  const double *bcol = c < kb ? colp(B, c) : nullptr;
+  const double *bcol = colp(B, c < kb ? c : kb - 1) + 2 * g;
 
   d4 acc[MAXT];
 #pragma unroll
@@ -164,24 +169,17 @@ __global__ __launch_bounds__(256) void k_gemm_tn(MvDesc A, int L, MvDesc B, int 
 
   for (long long ch = wid; ch < nchunks; ch += nw) {
     const long long r0 = ch * TN_ROWS;
-    const bool full = r0 + TN_ROWS <= nrows;
-    auto ld2 = [&](const double *p, long long r) -> d2 {
-      if (!p) return d2{0.0, 0.0};
-      if (full) return *(const d2 *)(p + r);
-      return d2{r < nrows ? p[r] : 0.0, r + 1 < nrows ? p[r + 1] : 0.0};
-    };
-    d2 bq[8];
+    d2 bq[8], cur[8], nxt[8];
 #pragma unroll
-    for (int p = 0; p < 8; ++p) bq[p] = ld2(bcol, r0 + 8 * p + 2 * g);
-    d2 cur[8], nxt[8];
+    for (int p = 0; p < 8; ++p) bq[p] = *(const d2 *)(bcol + r0 + 8 * p);
 #pragma unroll
-    for (int p = 0; p < 8; ++p) cur[p] = ld2(acol[0], r0 + 8 * p + 2 * g);
+    for (int p = 0; p < 8; ++p) cur[p] = *(const d2 *)(acol[0] + r0 + 8 * p);
 #pragma unroll
     for (int tt = 0; tt < MAXT; ++tt) {
       if (tt < nt) {
         if (tt + 1 < nt) {
 #pragma unroll
-          for (int p = 0; p < 8; ++p) nxt[p] = ld2(acol[tt + 1], r0 + 8 * p + 2 * g);
+          for (int p = 0; p < 8; ++p) nxt[p] = *(const d2 *)(acol[tt + 1] + r0 + 8 * p);
         }
 #pragma unroll
         for (int p = 0; p < 8; ++p) {
@@ -286,6 +284,38 @@ __global__ __launch_bounds__(256) void k_reduce(const double *__restrict__ parti
   red[s][l] = (a0 + a1) + (a2 + a3);
   __syncthreads();
   if (s == 0 && o < nout) out[o] = alpha * ((red[0][l] + red[1][l]) + (red[2][l] + red[3][l]));
+}
+
+__global__ __launch_bounds__(256) void k_reduce_ld(const double *__restrict__ partial, int nblocks,
+                                                   int rows, int nout, int ldo, double alpha,
+                                                   double *__restrict__ out) {
+  __shared__ double red[4][64];
+  const int l = threadIdx.x & 63, s = threadIdx.x >> 6;
+  const int o = blockIdx.x * 64 + l;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  if (o < nout) {
+    int b = s;
+    for (; b + 12 < nblocks; b += 16) {
+      a0 += partial[(long long)b * nout + o];
+      a1 += partial[(long long)(b + 4) * nout + o];
+      a2 += partial[(long long)(b + 8) * nout + o];
+      a3 += partial[(long long)(b + 12) * nout + o];
+    }
+    for (; b < nblocks; b += 4) a0 += partial[(long long)b * nout + o];
+  }
+  red[s][l] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (s == 0 && o < nout)
+    out[(o % rows) + (long long)(o / rows) * ldo] =
+        alpha * ((red[0][l] + red[1][l]) + (red[2][l] + red[3][l]));
+}
+
+void launch_reduce_partials_ld(hipStream_t s, const double *partial, int nblocks, int rows, int cols,
+                               int ldo, double alpha, double *out) {
+  const int nout = rows * cols;
+  if (nout <= 0) return;
+  k_reduce_ld<<<cdiv(nout, 64), 256, 0, s>>>(partial, nblocks, rows, nout, ldo, alpha, out);
+  LAUNCH_CHECK();
 }
 
 void launch_reduce_partials(hipStream_t s, const double *partial, int nblocks, int nout,

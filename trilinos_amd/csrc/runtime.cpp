@@ -59,7 +59,8 @@ void migmres_ctx::allreduce(double *d, size_t n, bool max) {
 }
 
 const char *kKernelClassNames[K_NUM_CLASSES] = {"spmm", "gemm_tn", "reduce", "gemm_nn", "coldot",
-                                                "axpby", "scale", "fill", "copy", "random", "pack"};
+                                                "axpby", "scale", "fill", "copy", "random", "pack",
+                                                "findbasis"};
 
 hipEvent_t migmres_ctx::get_event() {
   if (!event_pool.empty()) {
@@ -130,6 +131,47 @@ extern "C" const char *migmres_kernel_class_name(int i) {
   return (i >= 0 && i < K_NUM_CLASSES) ? kKernelClassNames[i] : "";
 }
 
+void *migmres_ctx::dev_alloc(size_t bytes, size_t *rounded) {
+  const size_t gran = bytes >= (64u << 20) ? (2u << 20) : 4096;
+  const size_t r = (bytes + gran - 1) / gran * gran;
+  for (size_t i = 0; i < pool.size(); ++i)
+    if (pool[i].first == r) {
+      void *p = pool[i].second;
+      pool.erase(pool.begin() + (long)i);
+      pool_bytes -= r;
+      *rounded = r;
+      return p;
+    }
+  void *p = nullptr;
+  hipError_t e = hipMalloc(&p, r);
+  if (e != hipSuccess) {  // release cached blocks and retry once
+    (void)hipGetLastError();
+    pool_trim();
+    e = hipMalloc(&p, r);
+  }
+  if (e != hipSuccess) throw Error(MIGMRES_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+  *rounded = r;
+  return p;
+}
+
+void migmres_ctx::dev_free(void *p, size_t rounded) {
+  if (!p) return;
+  pool.emplace_back(rounded, p);
+  pool_bytes += rounded;
+}
+
+void migmres_ctx::pool_trim() {
+  (void)hipStreamSynchronize(stream);
+  for (auto &b : pool) (void)hipFree(b.second);
+  pool.clear();
+  pool_bytes = 0;
+}
+
+void migmres_ctx::allreduce_async(double *d, size_t n) {
+  if (nranks == 1 || n == 0) return;
+  MIG_NCCL(ncclAllReduce(d, d, n, ncclDouble, ncclSum, comm, stream));
+}
+
 extern "C" int migmres_comm_unique_id(unsigned char out[128]) {
   return guard([&] {
     ncclUniqueId id;
@@ -168,6 +210,8 @@ extern "C" int migmres_ctx_destroy(migmres_ctx *c) {
   return guard([&] {
     if (!c) return;
     hipStreamSynchronize(c->stream);
+    c->pool_trim();
+    for (auto e : c->event_pool) (void)hipEventDestroy(e);
     if (c->comm) ncclCommDestroy(c->comm);
     if (c->d_partial) hipFree(c->d_partial);
     if (c->d_red) hipFree(c->d_red);
@@ -205,7 +249,7 @@ extern "C" int migmres_ctx_sum_all(migmres_ctx *c, const double *in, double *out
 // ------------------------------------------------------------------------------------
 migmres_mv::~migmres_mv() {
   if (d_cols) hipFree(d_cols);
-  if (owner && base) hipFree(base);
+  if (owner && base) ctx->dev_free(base, alloc_bytes);
 }
 
 namespace migmres {
@@ -220,10 +264,19 @@ migmres_mv *mv_create(migmres_ctx *ctx, long long n_global, int n_local, int nco
   m->ld = round_up(n_local > 0 ? n_local : 1, 64);
   m->owner = true;
   const size_t bytes = (size_t)m->ld * (size_t)(ncols > 0 ? ncols : 1) * sizeof(double) + 256;
-  hipError_t e = hipMalloc(&m->base, bytes);
+  try {
+    m->base = (double *)ctx->dev_alloc(bytes, &m->alloc_bytes);
+  } catch (...) {
+    m->owner = false;
+    delete m;
+    throw;
+  }
+  // Invariant used by the streaming kernels: padding rows [n_local, ld) stay zero (no
+  // kernel writes past n_local), so full 64-row chunks can be read unguarded.
+  hipError_t e = hipMemsetAsync(m->base, 0, bytes, ctx->stream);
   if (e != hipSuccess) {
     delete m;
-    throw Error(MIGMRES_ENOMEM, std::string("hipMalloc multivector: ") + hipGetErrorString(e));
+    throw Error(MIGMRES_EHIP, std::string("hipMemset multivector: ") + hipGetErrorString(e));
   }
   return m;
 }

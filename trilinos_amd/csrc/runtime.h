@@ -12,7 +12,7 @@
 
 // Per-kernel-class profiling with HIP events on the context stream (bench.py roofline).
 enum KernelClass { K_SPMM = 0, K_GEMM_TN, K_REDUCE, K_GEMM_NN, K_COLDOT, K_AXPBY, K_SCALE, K_FILL,
-                   K_COPY, K_RANDOM, K_PACK, K_NUM_CLASSES };
+                   K_COPY, K_RANDOM, K_PACK, K_FB, K_NUM_CLASSES };
 extern const char *kKernelClassNames[K_NUM_CLASSES];
 
 struct migmres_ctx;
@@ -41,6 +41,13 @@ struct migmres_ctx {
   long long prof_count[K_NUM_CLASSES] = {};
   hipEvent_t get_event();
   void prof_collect();
+  // Caching device allocator: freed blocks are kept per (rounded) size and reused, so the
+  // multi-GB Krylov basis is not re-mapped on every solve.
+  std::vector<std::pair<size_t, void *>> pool;
+  size_t pool_bytes = 0;
+  void *dev_alloc(size_t bytes, size_t *rounded);
+  void dev_free(void *p, size_t rounded);
+  void pool_trim();
   hipStream_t stream = nullptr;
   ncclComm_t comm = nullptr;
   // device scratch: per-workgroup partials, reduced results, staged coefficients
@@ -60,10 +67,13 @@ struct migmres_ctx {
   double *pinned(size_t n);
   // In-place sum (or max) all-reduce of n device doubles on the context stream.
   void allreduce(double *d, size_t n, bool max = false);
+  // Stream-ordered sum all-reduce (no host synchronisation).
+  void allreduce_async(double *d, size_t n);
 };
 
 struct migmres_mv {
   migmres_ctx *ctx = nullptr;
+  size_t alloc_bytes = 0;
   long long n_global = 0;
   int n_local = 0;
   int ncols = 0;

@@ -17,6 +17,7 @@
 #include <memory>
 #include <string>
 
+#include "icgs.h"
 #include "runtime.h"
 
 using namespace migmres;
@@ -241,6 +242,233 @@ struct Icgs {
 };
 
 // ------------------------------------------------------------------------------------
+// Device-resident ICGS (same operation sequence as Icgs above; coefficients and
+// decisions stay on the device, one host synchronisation per call).  Falls back to the
+// host-driven Icgs -- from the saved input block -- whenever the reference would leave
+// the fast path (blkOrtho dependency, findBasis rank deficiency).
+// ------------------------------------------------------------------------------------
+struct FastIcgs {
+  migmres_ctx *ctx = nullptr;
+  Icgs *slow = nullptr;
+  int n_local = 0, kmax = 0, Lmax = 0;
+  long long n_global = 0;
+  int nblk_tn = 1, nblk_ic = 1;
+  double *partial = nullptr, *R1 = nullptr, *R2 = nullptr, *Cout = nullptr, *red = nullptr, *S = nullptr;
+  IcgsState *st = nullptr;
+  double *h = nullptr;  // pinned: state + C
+  MvPtr tmpX;
+  long long calls = 0, fallbacks = 0;
+
+  ~FastIcgs() { release(); }
+  void release() {
+    if (ctx) hipStreamSynchronize(ctx->stream);
+    for (void *p : {(void *)partial, (void *)R1, (void *)R2, (void *)Cout, (void *)red, (void *)S, (void *)st})
+      if (p) hipFree(p);
+    if (h) hipHostFree(h);
+    partial = R1 = R2 = Cout = red = S = nullptr;
+    st = nullptr;
+    h = nullptr;
+    tmpX.reset();
+  }
+
+  bool supports(int k) const { return k >= 1 && k <= 16; }
+
+  void setup(migmres_ctx *c, long long ng, int nl, int k, int lmax) {
+    if (ctx == c && n_local == nl && n_global == ng && k <= kmax && lmax <= Lmax) return;
+    release();
+    ctx = c;
+    n_global = ng;
+    n_local = nl;
+    kmax = k;
+    Lmax = lmax;
+    nblk_tn = gemm_tn_blocks(nl);
+    nblk_ic = icgs_blocks(nl);
+    const size_t np = std::max((size_t)nblk_tn * 512 * 16, (size_t)nblk_ic * 17);
+    MIG_HIP(hipMalloc(&partial, sizeof(double) * np));
+    MIG_HIP(hipMalloc(&R1, sizeof(double) * (size_t)(lmax + k) * k));
+    MIG_HIP(hipMalloc(&R2, sizeof(double) * (size_t)(lmax + k) * k));
+    MIG_HIP(hipMalloc(&Cout, sizeof(double) * (size_t)(lmax + k) * k));
+    MIG_HIP(hipMalloc(&red, sizeof(double) * 64));
+    const size_t sbytes = sizeof(double) * ((size_t)(nl > 0 ? nl : 1) + 64);
+    MIG_HIP(hipMalloc(&S, sbytes));
+    MIG_HIP(hipMemset(S, 0, sbytes));  // zero padding row read by the row-pair kernels
+    MIG_HIP(hipMalloc(&st, sizeof(IcgsState)));
+    MIG_HIP(hipHostMalloc(&h, sizeof(IcgsState) + sizeof(double) * (size_t)(lmax + k) * k, hipHostMallocDefault));
+    tmpX = MvPtr(mv_create(c, ng, nl, k));
+  }
+
+  void allreduce(double *d, size_t n) {
+    if (ctx->nranks == 1 || n == 0) return;
+    ctx->allreduce_async(d, n);
+  }
+
+  // out (L x kb, leading dim ldo) = A^T B, summed over ranks.
+  void tn(const MvDesc &A, int L, const MvDesc &B, int kb, double *out, int ldo) {
+    for (int a0 = 0; a0 < L; a0 += 512) {
+      const int lc = std::min(512, L - a0);
+      MvDesc Ac = A;
+      Ac.ncols = lc;
+      if (A.cols)
+        Ac.cols = A.cols + a0;
+      else
+        Ac.base = A.base + (long long)a0 * A.ld;
+      {
+        ProfScope ps(ctx, K_GEMM_TN, 8.0 * n_local * (lc + kb) + 8.0 * nblk_tn * lc * kb);
+        launch_gemm_tn_partial(ctx->stream, Ac, lc, B, kb, n_local, partial, nblk_tn);
+      }
+      ProfScope ps(ctx, K_REDUCE, 8.0 * nblk_tn * lc * kb);
+      launch_reduce_partials_ld(ctx->stream, partial, nblk_tn, lc, kb, ldo, 1.0, out + a0);
+    }
+    if (ldo == L) allreduce(out, (size_t)L * kb);
+  }
+
+  void reduce_small(int nvals) {
+    ProfScope ps(ctx, K_REDUCE, 8.0 * nblk_ic * nvals);
+    launch_reduce_small(ctx->stream, partial, nblk_ic, nvals, red);
+    allreduce(red, (size_t)nvals);
+  }
+
+  void nn(const MvDesc &Q, int L, const double *M, int ldm, const MvDesc &X, int k, bool dot) {
+    if (!dot) {
+      ProfScope ps(ctx, K_GEMM_NN, 8.0 * n_local * (L + 2.0 * k));
+      launch_gemm_nn(ctx->stream, Q, L, M, ldm, X, n_local, -1.0, 1.0);
+      return;
+    }
+    ProfScope ps(ctx, K_GEMM_NN, 8.0 * n_local * (L + 2.0 * k));
+    launch_gemm_nn_dot(ctx->stream, Q, L, M, ldm, X, n_local, -1.0, 1.0, 1, X, partial, nblk_ic);
+  }
+
+  void find_basis(const MvDesc &X, int k, int complete) {
+    const double n = (double)n_local;
+    for (int j = 0; j < k; ++j) {
+      {
+        ProfScope ps(ctx, K_FB, 8.0 * n * (j + 1) + (j > 0 ? 8.0 * n : 0.0));
+        launch_fb_a(ctx->stream, X, j, st, n_local, partial, nblk_ic);
+      }
+      reduce_small(j + 1);
+      launch_fb_scalar(ctx->stream, st, red, 0, j, k, complete);
+      if (j == 0) continue;
+      {
+        ProfScope ps(ctx, K_FB, 8.0 * n * (j + 2));
+        launch_fb_b(ctx->stream, X, j, st, S, n_local, partial, nblk_ic);
+      }
+      reduce_small(j);
+      launch_fb_scalar(ctx->stream, st, red, 1, j, k, complete);
+      {
+        ProfScope ps(ctx, K_FB, 8.0 * n * (j + 3));
+        launch_fb_c(ctx->stream, X, j, st, S, n_local, partial, nblk_ic);
+      }
+      reduce_small(1);
+      launch_fb_scalar(ctx->stream, st, red, 2, j, k, complete);
+    }
+    ProfScope ps(ctx, K_SCALE, 16.0 * n);
+    launch_scale_col(ctx->stream, X, k - 1, st, n_local);
+  }
+
+  void fetch(int L, int k) {
+    MIG_HIP(hipMemcpyAsync(h, st, sizeof(IcgsState), hipMemcpyDeviceToHost, ctx->stream));
+    if (L > 0)
+      MIG_HIP(hipMemcpyAsync(h + sizeof(IcgsState) / sizeof(double), Cout, sizeof(double) * (size_t)L * k,
+                             hipMemcpyDeviceToHost, ctx->stream));
+    MIG_HIP(hipStreamSynchronize(ctx->stream));
+  }
+  const IcgsState &hst() const { return *reinterpret_cast<const IcgsState *>(h); }
+  const double *hC() const { return h + sizeof(IcgsState) / sizeof(double); }
+
+  void save_input(migmres_mv &X) {
+    ProfScope ps(ctx, K_COPY, 16.0 * n_local * X.ncols);
+    MvPtr t = view(*tmpX, 0, X.ncols);
+    launch_copy(ctx->stream, X.desc(), t->desc(), n_local);
+  }
+  void restore_input(migmres_mv &X) {
+    MvPtr t = view(*tmpX, 0, X.ncols);
+    launch_copy(ctx->stream, t->desc(), X.desc(), n_local);
+  }
+
+  // projectAndNormalize(X, [C], B, [Q]).
+  int project_and_normalize(migmres_mv &X, migmres_mv &Q, double *C, int ldc, double *B, int ldb) {
+    ++calls;
+    const int k = X.ncols, L = Q.ncols;
+    launch_state_reset(ctx->stream, st, slow->blk_tol, slow->sing_tol);
+    const MvDesc xd = X.desc(), qd = Q.desc();
+    if (k == 1) {  // blkOrtho1, then MvDot and MvScale
+      tn(qd, L, xd, 1, R1, L);
+      nn(qd, L, R1, L, xd, 1, false);
+      tn(qd, L, xd, 1, R2, L);
+      nn(qd, L, R2, L, xd, 1, true);
+      reduce_small(1);
+      launch_fb_scalar(ctx->stream, st, red, 4, 0, 1, 0);
+      {
+        ProfScope ps(ctx, K_SCALE, 16.0 * n_local);
+        launch_scale_col(ctx->stream, xd, 0, st, n_local);
+      }
+      launch_add_coef(ctx->stream, R1, L, R2, L, Cout, L, L, 1);
+      fetch(L, 1);
+      for (int i = 0; i < L; ++i) C[i] = hC()[i];
+      B[0] = hst().B[0];
+      return 1;
+    }
+    save_input(X);
+    // blkOrtho: oldDot comes from the Gram block of [Q X]^T X when Q and X are adjacent
+    const bool adjacent = Q.contiguous() && X.contiguous() && Q.ld == X.ld && X.base == Q.base + (long long)L * Q.ld;
+    if (adjacent) {
+      MvDesc qx = qd;
+      qx.ncols = L + k;
+      tn(qx, L + k, xd, k, R1, L + k);
+    } else {
+      tn(qd, L, xd, k, R1, L + k);
+      tn(xd, k, xd, k, R1 + L, L + k);
+      allreduce(R1, (size_t)(L + k) * k);
+    }
+    launch_blk_old(ctx->stream, st, R1, L + k, L, k);
+    nn(qd, L, R1, L + k, xd, k, false);
+    tn(qd, L, xd, k, R2, L);
+    nn(qd, L, R2, L, xd, k, true);
+    reduce_small(k);
+    launch_fb_scalar(ctx->stream, st, red, 3, 0, k, 0);
+    launch_add_coef(ctx->stream, R1, L + k, R2, L, Cout, L, L, k);
+    find_basis(xd, k, 0);
+    fetch(L, k);
+    const IcgsState &s = hst();
+    if (s.neg != 0.0) throw Error(MIGMRES_ESTATE, "ICGS: negative definiteness in inner product");
+    if (s.dep != 0.0 || s.failed >= 0) {
+      ++fallbacks;
+      restore_input(X);
+      const int rank = slow->blk_ortho_sing(X, Q, C, ldc, B, ldb);
+      MIG_HIP(hipStreamSynchronize(ctx->stream));
+      return rank;
+    }
+    for (int j = 0; j < k; ++j) {
+      for (int i = 0; i < L; ++i) C[i + (size_t)j * ldc] = hC()[i + (size_t)j * L];
+      for (int i = 0; i < k; ++i) B[i + (size_t)j * ldb] = s.B[i + 16 * j];
+    }
+    return k;
+  }
+
+  // normalize = findBasis(completeBasis = true)
+  int normalize(migmres_mv &X, double *B, int ldb) {
+    ++calls;
+    const int k = X.ncols;
+    launch_state_reset(ctx->stream, st, slow->blk_tol, slow->sing_tol);
+    save_input(X);
+    find_basis(X.desc(), k, 1);
+    fetch(0, k);
+    const IcgsState &s = hst();
+    if (s.neg != 0.0) throw Error(MIGMRES_ESTATE, "ICGS: negative definiteness in inner product");
+    if (s.failed >= 0) {
+      ++fallbacks;
+      restore_input(X);
+      const int rank = slow->normalize(X, B, ldb);
+      MIG_HIP(hipStreamSynchronize(ctx->stream));
+      return rank;
+    }
+    for (int j = 0; j < k; ++j)
+      for (int i = 0; i < k; ++i) B[i + (size_t)j * ldb] = s.B[i + 16 * j];
+    return k;
+  }
+};
+
+// ------------------------------------------------------------------------------------
 // Small dense helpers (Teuchos::BLAS semantics, column-major)
 // ------------------------------------------------------------------------------------
 void rotg(double &a, double &b, double &c, double &s) {
@@ -285,6 +513,8 @@ struct migmres_solver {
   migmres_ctx *ctx = nullptr;
   Params p;
   Icgs ortho;
+  FastIcgs fast;
+  bool use_fast = true;
   // results
   int num_iters = 0;
   double achieved_tol = 0.0;
@@ -293,6 +523,8 @@ struct migmres_solver {
   int hist_cols = 0;
   long long n_apply = 0, n_explicit = 0, n_restarts = 0, n_block_iters = 0;
   double t_total = 0, t_spmm = 0, t_ortho = 0, t_lsq = 0, t_comm = 0;
+  double t_check = 0, t_restart = 0, t_setup = 0;
+  bool sync_timers() const { return (p.verbosity & 1) != 0; }
 };
 
 namespace {
@@ -540,6 +772,12 @@ struct Engine {
   }
 
   bool check(Iter &it) {  // StatusTestCombo OR: both members evaluated
+    auto t0 = Clock::now();
+    struct T {
+      migmres_solver *S;
+      Clock::time_point t0;
+      ~T() { S->t_check += since(t0); }
+    } tm{S, t0};
     const bool a = max_iters_check(it);
     const bool b = imp_check(it);
     S->history.insert(S->history.end(), imp.testvector.begin(), imp.testvector.end());
@@ -623,6 +861,14 @@ struct Engine {
 
   struct OrthoFailure {};
 
+  int normalize(migmres_mv &V0, double *B, int ldb) {
+    auto t0 = Clock::now();
+    const int r = (S->use_fast && S->fast.supports(V0.ncols)) ? S->fast.normalize(V0, B, ldb)
+                                                             : S->ortho.normalize(V0, B, ldb);
+    S->t_ortho += since(t0);
+    return r;
+  }
+
   void iterate(Iter &it) {  // BlockGmresIter::iterate (BelosBlockGmresIter.hpp:659-766)
     const int k = it.k, search = k * it.nb;
     std::vector<double> subH, subH2;
@@ -637,7 +883,9 @@ struct Engine {
       subH.assign((size_t)lcl * k, 0.0);
       subH2.assign((size_t)k * k, 0.0);
       auto t0 = Clock::now();
-      const int rank = S->ortho.project_and_normalize(*Vnext, *Q, subH.data(), lcl, subH2.data(), k);
+      const int rank = S->use_fast && S->fast.supports(k)
+                           ? S->fast.project_and_normalize(*Vnext, *Q, subH.data(), lcl, subH2.data(), k)
+                           : S->ortho.project_and_normalize(*Vnext, *Q, subH.data(), lcl, subH2.data(), k);
       S->t_ortho += since(t0);
       for (int j = 0; j < k; ++j) {
         for (int i = 0; i < lcl; ++i) it.Rat(i, c + j) = subH[(size_t)i + (size_t)j * lcl];
@@ -675,6 +923,7 @@ struct Engine {
     while (to_solve > 0) {
       int nb = p.num_blocks;
       if ((long long)block * p.num_blocks > dim) nb = (int)(block == 1 ? dim / block : (dim - block) / block);
+      auto ts0 = Clock::now();
       Iter it;
       it.k = block;
       it.nb = nb;
@@ -693,9 +942,15 @@ struct Engine {
         mv_assign(*r0v, *V0);
       }
       std::vector<double> z0((size_t)block * block, 0.0);
-      if (S->ortho.normalize(*V0, z0.data(), block) != block)
+      if (S->use_fast && S->fast.supports(block)) {
+        S->fast.slow = &S->ortho;
+        S->fast.setup(lp.X->ctx, lp.X->n_global, lp.X->n_local, block, it.sd);
+      }
+      if (normalize(*V0, z0.data(), block) != block)
         throw Error(MIGMRES_ESTATE, "BlockGmresSolMgr: failed to compute initial block of orthonormal vectors");
       initialize(it, *V0, z0);
+      if (S->sync_timers()) MIG_HIP(hipStreamSynchronize(lp.X->ctx->stream));
+      S->t_setup += since(ts0);
       int restarts = 0;
       while (true) {
         try {
@@ -715,13 +970,15 @@ struct Engine {
               break;
             }
             ++restarts;
+            auto tr0 = Clock::now();
             MvPtr upd = current_update(it);
             if (upd.p) mv_add_mv(1.0, *lp.curX, 1.0, *upd, *lp.curX);
             lp.curr_res_vec(*V0);
             std::fill(z0.begin(), z0.end(), 0.0);
-            if (S->ortho.normalize(*V0, z0.data(), block) != block)
+            if (normalize(*V0, z0.data(), block) != block)
               throw Error(MIGMRES_ESTATE, "BlockGmresSolMgr: failed to compute initial block after restart");
             initialize(it, *V0, z0);
+            S->t_restart += since(tr0);
           } else {
             throw Error(MIGMRES_ESTATE, "BlockGmresSolMgr: invalid return from iterate()");
           }
@@ -835,7 +1092,7 @@ extern "C" int migmres_solver_solve(migmres_solver *s, migmres_crs *A, migmres_m
               "LinearProblem: inconsistent X/B/A shapes");
     s->history.clear();
     s->n_apply = s->n_explicit = s->n_restarts = s->n_block_iters = 0;
-    s->t_spmm = s->t_ortho = s->t_lsq = 0.0;
+    s->t_spmm = s->t_ortho = s->t_lsq = s->t_check = s->t_restart = s->t_setup = 0.0;
     const double comm0 = s->ctx->comm_seconds;
     auto t0 = Clock::now();
     Engine E(s, s->p.tol, s->p.max_iters);
@@ -876,8 +1133,8 @@ extern "C" int migmres_solver_counters(const migmres_solver *s, long long *out, 
 }
 extern "C" int migmres_solver_timers(const migmres_solver *s, double *out, int n) {
   return guard([&] {
-    const double v[5] = {s->t_total, s->t_spmm, s->t_ortho, s->t_lsq, s->t_comm};
-    for (int i = 0; i < n && i < 5; ++i) out[i] = v[i];
+    const double v[8] = {s->t_total, s->t_spmm, s->t_ortho, s->t_lsq, s->t_comm, s->t_check, s->t_restart, s->t_setup};
+    for (int i = 0; i < n && i < 8; ++i) out[i] = v[i];
   });
 }
 
