@@ -67,11 +67,27 @@ def cpu_baseline(k, nb, seconds):
                       f"in {t:.2f} s, scaled by 256^3/64^3 rows to the 256^3 workload"}
 
 
+def pmc_traffic(kernel_class, world):
+    """Per-launch HBM traffic of `kernel_class` from the committed rocprofv3 PMC summary
+    (profiles/pmc_summary.json, made by tools/pmc_summary.py from separate FETCH_SIZE and
+    WRITE_SIZE passes of this bench command, gfx950 corrections per MI355X_MICROARCH.md).
+    None when no summary for this configuration exists."""
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    if world != 1 or not os.path.exists(path):
+        return None
+    try:
+        summ = json.load(open(path))
+        ent = summ["kernels"].get(kernel_class)
+        return None if ent is None else ent["traffic_bytes_per_launch"]
+    except Exception:
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=25)
     ap.add_argument("--nx", type=int, default=256)
     ap.add_argument("--k", type=int, default=8)
     ap.add_argument("--nb", type=int, default=25)
@@ -142,7 +158,7 @@ def main():
         import ctypes as C
         call("migmres_ctx_profile", comm.h, 1)
         run(args.steps)
-        nk = 12
+        nk = 13
         ms, by, cnt = (C.c_double * nk)(), (C.c_double * nk)(), (C.c_longlong * nk)()
         call("migmres_ctx_profile_read", comm.h, ms, by, cnt, nk)
         call("migmres_ctx_profile", comm.h, 0)
@@ -171,8 +187,9 @@ def main():
         per_launch_bytes = st["bytes"] / st["launches"]
         per_launch_s = st["ms"] / 1e3 / st["launches"]
         ach = per_launch_bytes / per_launch_s / 1e9
+        traffic = pmc_traffic(dom, world)
         out["roofline"] = {"kernel": dom, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                           "frac": ach / HBM_PEAK_GBPS, "traffic": None,
+                           "frac": ach / HBM_PEAK_GBPS, "traffic": traffic,
                            "bytes_per_launch": per_launch_bytes, "mean_launch_us": per_launch_s * 1e6}
         out["kernels"] = {kname: dict(ms=v["ms"], launches=v["launches"],
                                       GBps=v["bytes"] / (v["ms"] / 1e3) / 1e9 if v["ms"] > 0 else None)

@@ -1,2 +1,6 @@
 source ./tools_gpu_check.sh
-step 300 tsolve.log python tools/time_solve.py 256
+export TMPDIR=/tmp
+step 900 bench.log python bench.py
+step 900 rocprof_stats.log rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof_r1 -o run -- python3 bench.py
+step 900 rocprof_fetch.log rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d gpurun_out/prof_r1_fetch -o run --kernel-include-regex "gemm_tn|gemm_nn|spmm|k_fb" -- python3 bench.py --no-cpu-baseline
+step 900 rocprof_write.log rocprofv3 --pmc WRITE_SIZE -T --output-format csv -d gpurun_out/prof_r1_write -o run --kernel-include-regex "gemm_tn|gemm_nn|spmm|k_fb" -- python3 bench.py --no-cpu-baseline

@@ -1,0 +1,85 @@
+"""Pin the oracle (oracle/) to the reference before trusting it.
+
+The reference cannot be built here under this task's rules (its build needs CMake-generated
+config headers and an external BLAS), so the oracle is pinned by:
+  * outputs of the real reference recorded in SURVEY.md section 6 (the example driver
+    belos/epetra/example/BlockGmres/BlockGmresEpetraGaleriEx.cpp, --nx=64 --num-rhs=8
+    --block-size=8 --ortho=ICGS --tol=1e-8 --max-subspace=50 --max-restarts=50):
+    201 iterations, 268 Epetra_CrsMatrix::Multiply calls, 4 restarts, 61 explicit-residual
+    checks (268 = 201 + 1 RHS product + 1 initial residual + 4 restarts + 61), true
+    relative residuals 3.5e-10 .. 9.9e-9;
+  * known-answer values that the reference's own unit tests hold (glibc rand(), MINSTD,
+    Epetra_MultiVector closed-form Norm1/Dot/Norm2 from
+    epetra/test/MultiVector/ExecuteTestProblems.cpp:227-272).
+"""
+
+import math
+
+import numpy as np
+import pytest
+
+from oracle import belos as ob, epetra as oe
+
+
+def test_glibc_rand_stream():
+    # glibc rand() without srand(): the stream the reference's std::rand() calls draw from
+    assert oe.glibc_rand(6) == [1804289383, 846930886, 1681692777, 1714636915, 1957747793, 424238335]
+
+
+def test_minstd_stream():
+    # Park-Miller minimal standard, seed 1 (Epetra_Util::RandomInt)
+    v, s = oe.minstd_stream(1, 3)
+    assert v.tolist() == [16807, 282475249, 1622650073] and s == 1622650073
+    assert oe.minstd_next(1) == 16807
+    # 10000th value of MINSTD from seed 1 is 1043618065 (Park & Miller 1988)
+    v, _ = oe.minstd_stream(1, 10000)
+    assert int(v[-1]) == 1043618065
+
+
+def test_epetra_multivector_closed_forms():
+    """ExecuteTestProblems.cpp:227-272: A[j][i] = i+1 (i < 9), A[j][9] = 10 + j."""
+    L, nv = 10, 4
+    A = np.zeros((L, nv))
+    for j in range(nv):
+        A[:L - 1, j] = np.arange(1, L)
+        A[L - 1, j] = L + j
+    dl = float(L)
+    norm1 = (dl - 1) * dl / 2 + A[L - 1]
+    dot = (dl - 1) * dl * (2 * (dl - 1) + 1) / 6 + A[L - 1] ** 2
+    np.testing.assert_allclose(np.abs(A).sum(0), norm1, rtol=0, atol=1e-12)
+    np.testing.assert_allclose(np.einsum("ij,ij->j", A, A), dot, rtol=0, atol=1e-12)
+    np.testing.assert_allclose(np.linalg.norm(A, axis=0), np.sqrt(dot), rtol=1e-15)
+
+
+def test_galeri_laplace3d_structure():
+    """nnz = 7 m^3 - 6 m^2 (SURVEY.md 8 sizes table); rows sorted by local column."""
+    m = 6
+    rp, gc, vv = oe.laplace3d_rows(m, m, m, 0, m ** 3)
+    assert rp[-1] == 7 * m ** 3 - 6 * m ** 2
+    D = oe.DistCrs(lambda f, c: oe.laplace3d_rows(m, m, m, f, c), m ** 3, 1)
+    rp, lc, lv = D.crs[0]
+    r = 2 * m * m + m + 2  # an interior row: below, lower, left, diag, right, upper, above
+    assert lc[rp[r]:rp[r + 1]].tolist() == [r - m * m, r - m, r - 1, r, r + 1, r + m, r + m * m]
+    assert lv[rp[r]:rp[r + 1]].tolist() == [-1.0, -1.0, -1.0, 6.0, -1.0, -1.0, -1.0]
+
+
+def test_reference_run_64cube_icgs():
+    """The recorded reference run reproduced by the oracle."""
+    m, k = 64, 8
+    n = m ** 3
+    # Xexact is the 3rd Epetra_MultiVector of the driver (B, X, Xexact), each consuming two
+    # rand() calls (Epetra_Util ctor + AllocateForCopy, Epetra_MultiVector.cpp:263-265)
+    seed = oe.glibc_rand(6)[5]
+    A = oe.DistCrs(lambda f, c: oe.laplace3d_rows(m, m, m, f, c), n, 1)
+    Xex, _ = oe.epetra_random_mv(seed, n, k)
+    B = A.apply(Xex)
+    res = ob.solve(A.apply, B, {"Num Blocks": 50, "Block Size": 8, "Maximum Iterations": n // 8 - 1,
+                                "Maximum Restarts": 50, "Convergence Tolerance": 1e-8,
+                                "Orthogonalization": "ICGS"})
+    assert res["converged"]
+    assert res["iterations"] == 201
+    assert res["n_apply"] + 1 == 268
+    assert res["restarts"] == 4
+    assert res["n_explicit"] == 61
+    rel = np.linalg.norm(B - A.apply(res["X"]), axis=0) / np.linalg.norm(B, axis=0)
+    assert f"{rel.min():.1e}" == "3.5e-10" and f"{rel.max():.1e}" == "9.9e-09"

@@ -60,7 +60,7 @@ void migmres_ctx::allreduce(double *d, size_t n, bool max) {
 
 const char *kKernelClassNames[K_NUM_CLASSES] = {"spmm", "gemm_tn", "reduce", "gemm_nn", "coldot",
                                                 "axpby", "scale", "fill", "copy", "random", "pack",
-                                                "findbasis"};
+                                                "findbasis", "gemm_nn_dot"};
 
 hipEvent_t migmres_ctx::get_event() {
   if (!event_pool.empty()) {

@@ -12,7 +12,7 @@
 
 // Per-kernel-class profiling with HIP events on the context stream (bench.py roofline).
 enum KernelClass { K_SPMM = 0, K_GEMM_TN, K_REDUCE, K_GEMM_NN, K_COLDOT, K_AXPBY, K_SCALE, K_FILL,
-                   K_COPY, K_RANDOM, K_PACK, K_FB, K_NUM_CLASSES };
+                   K_COPY, K_RANDOM, K_PACK, K_FB, K_GEMM_NN_DOT, K_NUM_CLASSES };
 extern const char *kKernelClassNames[K_NUM_CLASSES];
 
 struct migmres_ctx;

@@ -334,7 +334,7 @@ struct FastIcgs {
       launch_gemm_nn(ctx->stream, Q, L, M, ldm, X, n_local, -1.0, 1.0);
       return;
     }
-    ProfScope ps(ctx, K_GEMM_NN, 8.0 * n_local * (L + 2.0 * k));
+    ProfScope ps(ctx, K_GEMM_NN_DOT, 8.0 * n_local * (L + 2.0 * k));
     launch_gemm_nn_dot(ctx->stream, Q, L, M, ldm, X, n_local, -1.0, 1.0, 1, X, partial, nblk_ic);
   }
 
