@@ -158,7 +158,7 @@ def main():
         import ctypes as C
         call("migmres_ctx_profile", comm.h, 1)
         run(args.steps)
-        nk = 13
+        nk = 32  # more than the library's kernel classes; unused slots read back as 0
         ms, by, cnt = (C.c_double * nk)(), (C.c_double * nk)(), (C.c_longlong * nk)()
         call("migmres_ctx_profile_read", comm.h, ms, by, cnt, nk)
         call("migmres_ctx_profile", comm.h, 0)

@@ -102,6 +102,14 @@ int migmres_plan_local_crs(long long first, int n_local, const long long *rowptr
                            const long long *gcols, const double *vals, const long long *colmap,
                            int n_cols, int *lcols_out, double *vals_out);
 
+/* Row-pair gather plan of the SpMM kernel (no reference counterpart: a device layout
+ * derived from the local CRS).  xcols are X-space columns (owned column -> local row,
+ * remote -> n_local + ghost slot), rows sorted ascending.  Writes ptr[(n_local+1)/2 + 1],
+ * key[*nkeys] and meta[*nkeys] (pass NULL outputs to query *nkeys; *ok = 0 when the matrix
+ * does not fit the plan and the row-per-thread kernel is used instead). */
+int migmres_plan_pairs(int n_local, const long long *rowptr, const int *xcols, int *ptr_out,
+                       int *key_out, unsigned short *meta_out, long long *nkeys, int *ok);
+
 /* ---------------- CRS operator (Epetra_CrsMatrix / Tpetra::CrsMatrix) ---------------- */
 
 /* Collective over the context's ranks: builds the column map, local indices, the

@@ -52,6 +52,28 @@ def test_spmm_bit_exact(comm, kind, dims, k):
     np.testing.assert_allclose(Yd.download(), 2.0 * Aor.apply(X) - 0.5 * Y0, rtol=1e-15, atol=1e-14)
 
 
+@pytest.mark.parametrize("per_row,k,pairs", [(4, 8, "default"), (5, 3, "default"), (12, 8, "default"),
+                                              (7, 8, "off")])
+def test_spmm_unstructured_bit_exact(comm, per_row, k, pairs, monkeypatch):
+    """Unstructured rows through both SpMM kernels: the row-pair kernel (rows of <= 8
+    entries whose pairs need <= 12 keys) and the row-per-thread kernel (longer rows, or the
+    pair plan switched off with MIGMRES_NO_PAIR_SPMM=1)."""
+    import trilinos_amd as ta
+    from oracle import epetra as oe
+    from tests.test_plans import random_rows
+    if pairs == "off":
+        monkeypatch.setenv("MIGMRES_NO_PAIR_SPMM", "1")
+    n = 3001
+    rp, gc, vv = random_rows(n, 0, n, 29, per_row=per_row)
+    A = ta.CrsMatrix(comm, n, rp, gc, vv)
+    Aor = oe.DistCrs(lambda f, m: random_rows(n, f, m, 29, per_row=per_row), n, 1)
+    X, _ = oe.epetra_random_mv(11, n, k)
+    Xd = _upload(ta, comm, X)
+    Yd = ta.MultiVector(comm, n, k)
+    A.apply(Xd, Yd)
+    assert np.array_equal(Yd.download(), Aor.apply(X))
+
+
 @pytest.mark.parametrize("n,L,kb", [(1, 1, 1), (63, 5, 3), (64, 16, 16), (1000, 37, 8), (5000, 104, 8),
                                     (4097, 208, 8), (3001, 300, 16), (2049, 600, 20)])
 def test_trans_mv_mfma(comm, n, L, kb):

@@ -118,3 +118,99 @@ def test_uniform_map_remainder_rule():
     assert [oe.uniform_map(7, 4, p) for p in range(4)] == [(0, 2), (2, 2), (4, 2), (6, 1)]
     ids = np.arange(10)
     np.testing.assert_array_equal(oe.owner_of(ids, 10, 3), [0, 0, 0, 0, 1, 1, 1, 2, 2, 2])
+
+
+def xspace_cols(plan, first, nloc):
+    """Local CRS columns in the SpMM kernels' X space (owned -> local row, remote ->
+    n_local + ghost slot), as crs_create builds them."""
+    cm = plan["colmap"]
+    xs = np.full(cm.size, -1, dtype=np.int64)
+    own = (cm >= first) & (cm < first + nloc)
+    xs[own] = cm[own] - first
+    xs[plan["remote_lids"]] = nloc + np.arange(len(plan["remote_lids"]))
+    return xs[plan["lcols"]].astype(np.int32)
+
+
+def lib_pair_plan(nloc, rowptr, xcols):
+    L = _lib()
+    rowptr = np.ascontiguousarray(rowptr, dtype=np.int64)
+    xcols = np.ascontiguousarray(xcols, dtype=np.int32)
+    nk, ok = C.c_longlong(), C.c_int()
+    L.call("migmres_plan_pairs", nloc, L.lptr(rowptr), L.iptr(xcols), None, None, None, C.byref(nk), C.byref(ok))
+    if not ok.value:
+        return None
+    ptr = np.empty((nloc + 1) // 2 + 1, dtype=np.int32)
+    key = np.empty(nk.value, dtype=np.int32)
+    meta = np.empty(nk.value, dtype=np.uint16)
+    L.call("migmres_plan_pairs", nloc, L.lptr(rowptr), L.iptr(xcols), L.iptr(ptr), L.iptr(key),
+           meta.ctypes.data_as(C.POINTER(C.c_uint16)), C.byref(nk), C.byref(ok))
+    return ptr, key, meta
+
+
+def replay_pair_plan(nloc, ptr, key, meta):
+    """Per row, the (entry index, X-space column) sequence in which k_spmm_pair adds the
+    products: keys in plan order, low half before high half."""
+    seq = [[] for _ in range(nloc)]
+    for p in range(len(ptr) - 1):
+        for u in range(ptr[p], ptr[p + 1]):
+            k = int(key[u])
+            for h in range(2):
+                row = 2 * p + h
+                for half in range(2):
+                    idx = (int(meta[u]) >> (4 * (2 * h + half))) & 0xF
+                    if idx == 0xF:
+                        continue
+                    col = 2 * k + half if k >= 0 else nloc + 2 * (-k - 1) + half
+                    seq[row].append((idx, col))
+    return seq
+
+
+@pytest.mark.parametrize("kind,dims,P", CASES)
+def test_pair_plan_replays_stored_order(kind, dims, P):
+    """The row-pair SpMM plan visits every row's entries exactly in stored order, so its
+    sums (products v*x, no FMA) are the reference's bit for bit; matrices it cannot
+    express (rows longer than 8, more than 12 keys per pair) get no plan."""
+    nx, ny, nz = dims
+    n_global = nx * ny * nz
+    if kind == "Laplace2D":
+        gen = lambda f, m: oe.laplace2d_rows(nx, ny, f, m)  # noqa: E731
+    elif kind == "Laplace3D":
+        gen = lambda f, m: oe.laplace3d_rows(nx, ny, nz, f, m)  # noqa: E731
+    else:
+        gen = lambda f, m: random_rows(n_global, f, m, 17, per_row=5)  # noqa: E731
+    for p in range(P):
+        first, nloc = oe.uniform_map(n_global, P, p)
+        rp, gc, vv = gen(first, nloc)
+        plan = lib_plan(n_global, P, p, rp, gc, vv)
+        xc = xspace_cols(plan, first, nloc)
+        res = lib_pair_plan(nloc, rp, xc)
+        rp = np.asarray(rp, dtype=np.int64)
+        if kind == "random":
+            # 5-6 random columns per row: two rows rarely share pairs -> up to 12 keys
+            if res is None:
+                continue
+        assert res is not None
+        ptr, key, meta = res
+        assert np.all(np.diff(ptr) <= 12)
+        seq = replay_pair_plan(nloc, ptr, key, meta)
+        for r in range(nloc):
+            ent = list(range(rp[r + 1] - rp[r]))
+            assert [i for i, _ in seq[r]] == ent, r
+            assert [c for _, c in seq[r]] == xc[rp[r]:rp[r + 1]].tolist(), r
+
+
+def test_pair_plan_rejects_long_rows_and_repeats():
+    # a 9-entry row cannot be planned
+    rp = np.array([0, 9, 10])
+    xc = np.array(list(range(9)) + [1], dtype=np.int32)
+    assert lib_pair_plan(2, rp, xc) is None
+    # a repeated column in a row cannot be planned
+    rp = np.array([0, 2, 3])
+    xc = np.array([1, 1, 0], dtype=np.int32)
+    assert lib_pair_plan(2, rp, xc) is None
+    # odd row count: the last pair has one row
+    rp = np.array([0, 2, 3, 5])
+    xc = np.array([0, 2, 1, 0, 2], dtype=np.int32)
+    ptr, key, meta = lib_pair_plan(3, rp, xc)
+    seq = replay_pair_plan(3, ptr, key, meta)
+    assert seq == [[(0, 0), (1, 2)], [(0, 1)], [(0, 0), (1, 2)]]

@@ -5,6 +5,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <cmath>
 #include <vector>
 
 #include "../trilinos_amd/csrc/icgs.h"
@@ -53,7 +54,7 @@ int main(int argc, char **argv) {
   const int k = 8, Lmax = 216;
   double *V, *P, *R, *S;
   CK(hipMalloc(&V, sizeof(double) * ld * Lmax + 256));
-  CK(hipMalloc(&P, sizeof(double) * 4096 * 512 * 16));
+  CK(hipMalloc(&P, sizeof(double) * 4096 * 512 * 16 + sizeof(double) * 2048 * 256 * 16));
   CK(hipMalloc(&R, sizeof(double) * 512 * 16));
   CK(hipMalloc(&S, sizeof(double) * ld));
   fill<<<(ld * Lmax + 255) / 256, 256>>>(V, ld * Lmax, 1);
@@ -73,8 +74,46 @@ int main(int argc, char **argv) {
     const int nb2 = icgs_blocks((int)n);
     double t_nnd = timeit([&] { launch_gemm_nn_dot(s, Q, L, R, L + k, X, (int)n, -1.0, 1.0, 1, X, P, nb2); });
     const double by_nn = 8.0 * n * (L + 2 * k);
-    printf("L=%3d  tn %7.3f ms %6.0f GB/s | reduce %6.1f us | nn %7.3f ms %6.0f GB/s | nn_dot %7.3f ms %6.0f GB/s\n", L,
-           t_tn, by_tn / t_tn / 1e6, t_red * 1e3, t_nn, by_nn / t_nn / 1e6, t_nnd, by_nn / t_nnd / 1e6);
+    const int nbf = nn_tn_blocks((int)n, L);
+    double t_f = timeit([&] { launch_nn_tn(s, Q, L, R, L + k, X, (int)n, P, nbf); });
+    printf("L=%3d  tn %7.3f ms %6.0f GB/s | reduce %6.1f us | nn %7.3f ms %6.0f GB/s | nn_dot %7.3f ms %6.0f GB/s"
+           " | nn_tn %7.3f ms %6.0f GB/s (%d wg)\n", L,
+           t_tn, by_tn / t_tn / 1e6, t_red * 1e3, t_nn, by_nn / t_nn / 1e6, t_nnd, by_nn / t_nnd / 1e6, t_f,
+           by_nn / t_f / 1e6, nbf);
+  }
+  // correctness of the fused update+projection against nn followed by tn (L = 200, 40, 13)
+  for (int L : {200, 40, 13}) {
+    double *Xb, *R2a, *R2b;
+    CK(hipMalloc(&Xb, sizeof(double) * ld * k));
+    CK(hipMalloc(&R2a, sizeof(double) * L * k));
+    CK(hipMalloc(&R2b, sizeof(double) * L * k));
+    MvDesc Q{V, ld, nullptr, L};
+    MvDesc X{V + (long long)L * ld, ld, nullptr, k};
+    MvDesc XB{Xb, ld, nullptr, k};
+    fill<<<(ld * Lmax + 255) / 256, 256>>>(V, ld * Lmax, 7);
+    for (int c = 0; c < Lmax; ++c) CK(hipMemset(V + (long long)c * ld + n, 0, sizeof(double) * (ld - n)));
+    fill<<<((L + k) * k + 255) / 256, 256>>>(R, (long long)(L + k) * k, 3);
+    CK(hipMemcpy(Xb, X.base, sizeof(double) * ld * k, hipMemcpyDeviceToDevice));
+    launch_gemm_nn(s, Q, L, R, L + k, X, (int)n, -1.0, 1.0);
+    launch_gemm_tn_partial(s, Q, L, X, k, (int)n, P, nblk);
+    launch_reduce_partials_ld(s, P, nblk, L, k, L, 1.0, R2a);
+    const int nbf = nn_tn_blocks((int)n, L);
+    launch_nn_tn(s, Q, L, R, L + k, XB, (int)n, P, nbf);
+    launch_reduce_partials_ld(s, P, nbf, L, k, L, 1.0, R2b);
+    CK(hipDeviceSynchronize());
+    std::vector<double> xa((size_t)ld * k), xb((size_t)ld * k), ra(L * k), rb(L * k);
+    CK(hipMemcpy(xa.data(), X.base, sizeof(double) * ld * k, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(xb.data(), Xb, sizeof(double) * ld * k, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(ra.data(), R2a, sizeof(double) * L * k, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(rb.data(), R2b, sizeof(double) * L * k, hipMemcpyDeviceToHost));
+    double dx = 0, mx = 0, dr = 0, mr = 0;
+    for (size_t i = 0; i < xa.size(); ++i) dx = fmax(dx, fabs(xa[i] - xb[i])), mx = fmax(mx, fabs(xa[i]));
+    for (size_t i = 0; i < ra.size(); ++i) dr = fmax(dr, fabs(ra[i] - rb[i])), mr = fmax(mr, fabs(ra[i]));
+    printf("check nn_tn L=%d: X1 maxdiff %.3e (max %.3e)  R2 maxdiff %.3e (max %.3e)  %s\n", L, dx, mx, dr, mr,
+           (dx <= 1e-12 * mx && dr <= 1e-10 * mr) ? "OK" : "MISMATCH");
+    CK(hipFree(Xb));
+    CK(hipFree(R2a));
+    CK(hipFree(R2b));
   }
   // findBasis column kernels on the k-block
   IcgsState *st;

@@ -21,6 +21,11 @@ void launch_reduce_small(hipStream_t s, const double *partial, int nblocks, int 
 void launch_gemm_nn_dot(hipStream_t s, MvDesc A, int L, const double *M, int ldm, MvDesc X,
                         int nrows, double alpha, double beta, int dmode, MvDesc D, double *partial,
                         int nblocks);
+// X1 = X - Q C1 in place and per-workgroup partials of Q^T X1 (L x k, column-major).
+bool nn_tn_supported(int L, int k);
+int nn_tn_blocks(int nrows, int L);
+void launch_nn_tn(hipStream_t s, MvDesc Q, int L, const double *C1, int ldc, MvDesc X, int nrows,
+                  double *partial, int nblocks);
 void launch_fb_a(hipStream_t s, MvDesc X, int j, const IcgsState *st, int nrows, double *partial, int nb);
 void launch_fb_b(hipStream_t s, MvDesc X, int j, const IcgsState *st, double *S, int nrows, double *partial, int nb);
 void launch_fb_c(hipStream_t s, MvDesc X, int j, const IcgsState *st, const double *S, int nrows, double *partial,

@@ -180,6 +180,210 @@ void launch_gemm_nn_dot(hipStream_t s, MvDesc A, int L, const double *M, int ldm
 }
 
 // -------------------------------------------------------------------------------------
+// blkOrtho's first update fused with its second projection:
+//   X1 = X - Q C1 (in place)   and   partial[wg] = Q^T X1  (L x k per workgroup)
+// One pass over Q instead of two (the reference does MvTimesMatAddMv, then MvTransMv).
+// A workgroup stages a 16-row chunk of Q (all L <= 256 columns) in LDS, then
+//   phase 1: D = Qc C1 on MFMA (M = the 16 rows, K = Q columns split over the 4 waves,
+//            N = X columns; C1 register resident), waves summed in a fixed order -> X1,
+//   phase 2: acc += Qc^T X1 on MFMA (M = 16 Q columns per tile, K = the 16 rows),
+// while the loads of the next two chunks are in flight in registers (counted waits: the
+// loads are branch-free and the barriers are raw s_barrier, see lds_barrier()).
+// MFMA rather than VALU: the VALU form needs every lane to read whole C1 / X1 rows from
+// LDS (broadcast reads), which made it LDS-bound; here each lane reads one f64 per MFMA.
+// LDS: Qs[Lp][17] (odd stride: both phases' reads are conflict-free), Xs[16][16], red[3][4][64].
+// -------------------------------------------------------------------------------------
+typedef double d4_ __attribute__((ext_vector_type(4)));
+constexpr int NT_ROWS = 16, NT_MAXL = 256, NT_LDQ = 17;
+
+static size_t nt_lds_bytes(int L) {
+  const int Lp = (L + 15) & ~15;
+  return sizeof(double) * ((size_t)Lp * NT_LDQ + 256 + 3 * 256);
+}
+
+// Workgroup barrier for LDS hand-offs only.  __syncthreads()'s release fence waits for
+// vmcnt(0), which on gfx9 also counts stores: one global store before it would drain the
+// register prefetches that are meant to stay in flight across the barrier.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int NM>
+__global__ __launch_bounds__(256, 2) void k_nn_tn(MvDesc Q, int L, const double *__restrict__ C1, int ldc,
+                                                  MvDesc X, int k, int nrows, double *__restrict__ partial) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const int Lp = (L + 15) & ~15;
+  double *Qs = sm;
+  double *Xs = sm + (size_t)Lp * NT_LDQ;
+  double *red = Xs + 256;
+  const int t = threadIdx.x, w = t >> 6, l = t & 63, c = l & 15, g = l >> 4;
+  for (int e = t; e < (Lp - L) * NT_LDQ; e += 256) Qs[L * NT_LDQ + e] = 0.0;
+
+  // phase-1 B operand: C1[i = 4s + g][j = c] for the wave's K steps s = w + 4m
+  double b1[16];
+#pragma unroll
+  for (int m = 0; m < 16; ++m) {
+    const int i = 4 * (w + 4 * m) + g;
+    b1[m] = (i < L && c < k) ? C1[i + (long long)c * ldc] : 0.0;
+  }
+  d4_ acc2[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) acc2[m] = d4_{0.0, 0.0, 0.0, 0.0};
+
+  // loader: Q column lcol + 32 m (clamped to L - 1: duplicates rewrite the same value),
+  // rows lrow, lrow + 1 -- 8 lanes = one 128-B line.  Q is a contiguous column range.
+  const int lrow = 2 * (t & 7), lcol = t >> 3;
+  const double *qcol[NM];
+  int scol[NM];
+#pragma unroll
+  for (int m = 0; m < NM; ++m) {
+    const int i = lcol + 32 * m;
+    scol[m] = i < L ? i : L - 1;
+    qcol[m] = Q.base + (long long)scol[m] * Q.ld + lrow;
+  }
+  // wave 0 lane (g, c) updates X1[g + 4q][c], q < 4
+  const bool xl = c < k;
+  double *xcol = colp_(X, xl ? c : k - 1);
+  const long long nchunks = (nrows + NT_ROWS - 1) / NT_ROWS;
+  const long long G = gridDim.x;
+  auto clampc = [&](long long chunk) { return chunk < nchunks ? chunk : nchunks - 1; };
+  auto loadq = [&](d2(&p)[NM], long long chunk) {
+    chunk = clampc(chunk);
+#pragma unroll
+    for (int m = 0; m < NM; ++m) p[m] = *(const d2 *)(qcol[m] + chunk * NT_ROWS);
+  };
+  auto loadx = [&](double(&xv)[4], long long chunk) {
+    chunk = clampc(chunk);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) xv[q] = xcol[chunk * NT_ROWS + g + 4 * q];
+  };
+
+  // A chunk past the end (second half of the last 2-chunk step) runs the same instruction
+  // stream on clamped data with X1 = 0, adding nothing; keeping both halves unconditional
+  // keeps the wait counts static.
+  auto body = [&](d2(&p)[NM], double(&xv)[4], long long chunk) {
+    const bool live = chunk < nchunks;
+    const long long r0 = chunk * NT_ROWS;
+#pragma unroll
+    for (int m = 0; m < NM; ++m) {
+      Qs[scol[m] * NT_LDQ + lrow] = p[m].x;
+      Qs[scol[m] * NT_LDQ + lrow + 1] = p[m].y;
+    }
+    lds_barrier();
+    loadq(p, chunk + 2 * G);
+    // phase 1: this wave's share of D[r][j] = sum_i Q[r][i] C1[i][j], two MFMA chains
+    d4_ a1 = d4_{0.0, 0.0, 0.0, 0.0}, a2 = d4_{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int m = 0; m < 16; m += 2) {
+      const int s0 = w + 4 * m, s1 = w + 4 * (m + 1);
+      if (4 * s0 < L) a1 = __builtin_amdgcn_mfma_f64_16x16x4f64(Qs[(4 * s0 + g) * NT_LDQ + c], b1[m], a1, 0, 0, 0);
+      if (4 * s1 < L) a2 = __builtin_amdgcn_mfma_f64_16x16x4f64(Qs[(4 * s1 + g) * NT_LDQ + c], b1[m + 1], a2, 0, 0, 0);
+    }
+    a1 += a2;
+    if (w > 0) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) red[((w - 1) * 4 + q) * 64 + l] = a1[q];
+    }
+    lds_barrier();
+    if (w == 0) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = g + 4 * q;
+        const double d = (a1[q] + red[q * 64 + l]) + (red[(4 + q) * 64 + l] + red[(8 + q) * 64 + l]);
+        const double x1 = (xl && live) ? xv[q] - d : 0.0;
+        if (xl && live && r0 + r < nrows) xcol[r0 + r] = x1;
+        Xs[r * 16 + c] = x1;
+      }
+      loadx(xv, chunk + 2 * G);
+    }
+    lds_barrier();
+    // phase 2: acc[tile] += Q[:, tile]^T X1 over the chunk's 16 rows
+    double xb[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) xb[s] = Xs[(4 * s + g) * 16 + c];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int tt = w + 4 * m;
+      if (16 * tt < L) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          acc2[m] = __builtin_amdgcn_mfma_f64_16x16x4f64(Qs[(16 * tt + c) * NT_LDQ + 4 * s + g], xb[s], acc2[m],
+                                                         0, 0, 0);
+      }
+    }
+    lds_barrier();
+  };
+
+  d2 pa[NM], pb[NM];
+  double xa[4] = {0.0, 0.0, 0.0, 0.0}, xb2[4] = {0.0, 0.0, 0.0, 0.0};
+  const long long ch0 = blockIdx.x;
+  loadq(pa, ch0);
+  if (w == 0) loadx(xa, ch0);
+  asm volatile("" ::: "memory");  // keep pa's loads older than pb's (static wait counts in the loop)
+  loadq(pb, ch0 + G);
+  if (w == 0) loadx(xb2, ch0 + G);
+  for (long long ch = ch0; ch < nchunks; ch += 2 * G) {
+    body(pa, xa, ch);
+    body(pb, xb2, ch + G);
+  }
+  if (c < k) {
+    double *out = partial + (long long)blockIdx.x * L * k;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int tt = w + 4 * m;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = 16 * tt + g + 4 * q;
+        if (i < L) out[i + (long long)c * L] = acc2[m][q];
+      }
+    }
+  }
+}
+
+typedef void (*nt_kernel_t)(MvDesc, int, const double *, int, MvDesc, int, int, double *);
+
+static nt_kernel_t nt_pick(int L) {
+  switch ((L + 31) >> 5) {
+    case 1: return k_nn_tn<1>;
+    case 2: return k_nn_tn<2>;
+    case 3: return k_nn_tn<3>;
+    case 4: return k_nn_tn<4>;
+    case 5: return k_nn_tn<5>;
+    case 6: return k_nn_tn<6>;
+    case 7: return k_nn_tn<7>;
+    default: return k_nn_tn<8>;
+  }
+}
+
+int nn_tn_blocks(int nrows, int L) {
+  int per_cu = 0, dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nt_pick(L), 256, nt_lds_bytes(L)) != hipSuccess ||
+      per_cu < 1 || cus < 1) {
+    per_cu = 2;
+    cus = 256;
+  }
+  const long long nchunks = (nrows + NT_ROWS - 1) / NT_ROWS;
+  long long b = (long long)per_cu * cus;
+  if (b > nchunks) b = nchunks;
+  return b < 1 ? 1 : (int)b;
+}
+
+bool nn_tn_supported(int L, int k) { return L >= 1 && L <= NT_MAXL && k >= 1 && k <= 16; }
+
+void launch_nn_tn(hipStream_t s, MvDesc Q, int L, const double *C1, int ldc, MvDesc X, int nrows,
+                  double *partial, int nblocks) {
+  const int k = X.ncols;
+  if (!nn_tn_supported(L, k)) throw Error(MIGMRES_EINVAL, "nn_tn: 1 <= L <= 256 and 1 <= k <= 16");
+  if (Q.cols) throw Error(MIGMRES_EINVAL, "nn_tn: Q must be a contiguous column range");
+  hipLaunchKernelGGL(nt_pick(L), dim3(nblocks), dim3(256), nt_lds_bytes(L), s, Q, L, C1, ldc, X, k, nrows, partial);
+  LAUNCH_CHECK_();
+}
+
+// -------------------------------------------------------------------------------------
 // findBasis column kernels on the block X (nrows x k, k <= 16), column j.
 // -------------------------------------------------------------------------------------
 // Row pairs: each thread handles rows (r, r+1) with 16-byte loads; the padding row of a

@@ -67,6 +67,10 @@ struct MvDesc {
 // Y[:,c] = alpha * (A X)[:,c] + beta * Y[:,c] for the local CSR rows.  Column ids
 // >= n_local index the ghost block (column-major, leading dim ldg).  Row sums are
 // accumulated in stored order without contraction (Epetra GeneralMM order).
+// Row-pair SpMM (plan from make_pair_plan); vals padded by 8 entries, ghost ld even.
+void launch_spmm_pair(hipStream_t s, int n_local, int max_keys, const int *rowptr, const int *pptr,
+                      const int *pkey, const unsigned short *pmeta, const double *vals, MvDesc X,
+                      const double *ghost, long long ldg, MvDesc Y, double alpha, double beta);
 void launch_spmm(hipStream_t s, int row_begin, int row_end, const int *rowptr, const int *cols,
                  const double *vals, MvDesc X, int n_local, const double *ghost, long long ldg,
                  MvDesc Y, double alpha, double beta);

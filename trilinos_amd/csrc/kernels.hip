@@ -122,6 +122,124 @@ void launch_spmm(hipStream_t s, int row_begin, int row_end, const int *rowptr, c
 }
 
 // -------------------------------------------------------------------------------------
+// SpMM x k over row pairs (plan: make_pair_plan, plan.cpp).  One thread per row pair; every
+// X read is a 16-byte load of an aligned pair of rows shared by both rows of the pair (the
+// 8-byte gathers of k_spmm were instruction-bound: tools/mb_spmm.hip measured 1.35 ms
+// for 8-B gathers vs 0.79 ms for 16-B pair loads on the 256^3 stencil).  Each key's 16-bit
+// map says which entry of each row takes the low / high half; the row sums still run in
+// stored order with products v * x and no FMA, so the result is bit-identical to k_spmm.
+// Keys past a pair's count re-read the last key with an empty map (adds nothing).
+// -------------------------------------------------------------------------------------
+constexpr int PAIR_MAXR = 8;
+
+template <int KC, int PAIR_MAXK>
+__global__ __launch_bounds__(256) void k_spmm_pair(int npairs, const int *__restrict__ rowptr,
+                                                   const int *__restrict__ pptr, const int *__restrict__ pkey,
+                                                   const unsigned short *__restrict__ pmeta,
+                                                   const double *__restrict__ vals, MvDesc X, int n_local,
+                                                   const double *__restrict__ ghost, long long ldg, MvDesc Y,
+                                                   int c0, int kc, double alpha, double beta) {
+#pragma clang fp contract(off)
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= npairs) return;
+  const int ra = 2 * p;
+  const bool hasb = ra + 1 < n_local;
+  const int ea = rowptr[ra], eb = rowptr[ra + 1], ee = hasb ? rowptr[ra + 2] : eb;
+  double va[PAIR_MAXR], vb[PAIR_MAXR];
+#pragma unroll
+  for (int j = 0; j < PAIR_MAXR; ++j) {  // vals is padded by PAIR_MAXR entries
+    va[j] = vals[ea + j];
+    vb[j] = vals[eb + j];
+  }
+  (void)ee;
+  const int u0 = pptr[p], nu = pptr[p + 1] - u0;
+  int key[PAIR_MAXK];
+  double cx[PAIR_MAXK][4];  // coefficient taking (row a low, row a high, row b low, row b high)
+  unsigned long long use = 0;  // bit 4u + s: slot s of key u is used
+#pragma unroll
+  for (int u = 0; u < PAIR_MAXK; ++u) {
+    const int uu = u < nu ? u0 + u : u0 + (nu > 0 ? nu - 1 : 0);
+    key[u] = pkey[uu];
+    const unsigned m = u < nu ? pmeta[uu] : 0xFFFFu;
+#pragma unroll
+    for (int sl = 0; sl < 4; ++sl) {
+      const int idx = (m >> (4 * sl)) & 0xF;
+      double v = 0.0;
+#pragma unroll
+      for (int j = 0; j < PAIR_MAXR; ++j) v = (idx == j) ? (sl < 2 ? va[j] : vb[j]) : v;
+      cx[u][sl] = v;
+      use |= (idx != 0xF ? 1ull : 0ull) << (4 * u + sl);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < KC; ++c) {
+    if (c >= kc) break;
+    const double *xc = colp(X, c0 + c);
+    const double *gc = ghost + (long long)(c0 + c) * ldg;
+    double sa = 0.0, sb = 0.0;
+#pragma unroll
+    for (int u = 0; u < PAIR_MAXK; ++u) {
+      const int kk = key[u];
+      const double *src = kk >= 0 ? xc + 2LL * kk : gc + 2LL * (-kk - 1);
+      const d2 x = *(const d2 *)src;
+      const double pa0 = cx[u][0] * x.x, pa1 = cx[u][1] * x.y;
+      const double pb0 = cx[u][2] * x.x, pb1 = cx[u][3] * x.y;
+      sa = sa + ((use >> (4 * u)) & 1ull ? pa0 : 0.0);
+      sa = sa + ((use >> (4 * u + 1)) & 1ull ? pa1 : 0.0);
+      sb = sb + ((use >> (4 * u + 2)) & 1ull ? pb0 : 0.0);
+      sb = sb + ((use >> (4 * u + 3)) & 1ull ? pb1 : 0.0);
+    }
+    double *yp = colp(Y, c0 + c) + ra;
+    if (beta == 0.0) {
+      if (alpha != 1.0) {
+        sa = alpha * sa;
+        sb = alpha * sb;
+      }
+    } else {
+      sa = alpha * sa + beta * yp[0];
+      if (hasb) sb = alpha * sb + beta * yp[1];
+    }
+    if (hasb)
+      *(d2 *)yp = d2{sa, sb};
+    else
+      yp[0] = sa;
+  }
+}
+
+template <int MAXK>
+static void spmm_pair_cols(hipStream_t s, int npairs, const int *rowptr, const int *pptr, const int *pkey,
+                           const unsigned short *pmeta, const double *vals, MvDesc X, int n_local,
+                           const double *ghost, long long ldg, MvDesc Y, double alpha, double beta) {
+  const int k = Y.ncols;
+  const dim3 grid(cdiv(npairs, 256));
+  for (int c0 = 0; c0 < k; c0 += 8) {
+    const int kc = (k - c0) < 8 ? (k - c0) : 8;
+    if (kc == 1)
+      k_spmm_pair<1, MAXK><<<grid, 256, 0, s>>>(npairs, rowptr, pptr, pkey, pmeta, vals, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta);
+    else if (kc <= 2)
+      k_spmm_pair<2, MAXK><<<grid, 256, 0, s>>>(npairs, rowptr, pptr, pkey, pmeta, vals, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta);
+    else if (kc <= 4)
+      k_spmm_pair<4, MAXK><<<grid, 256, 0, s>>>(npairs, rowptr, pptr, pkey, pmeta, vals, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta);
+    else
+      k_spmm_pair<8, MAXK><<<grid, 256, 0, s>>>(npairs, rowptr, pptr, pkey, pmeta, vals, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta);
+    LAUNCH_CHECK();
+  }
+}
+
+void launch_spmm_pair(hipStream_t s, int n_local, int max_keys, const int *rowptr, const int *pptr,
+                      const int *pkey, const unsigned short *pmeta, const double *vals, MvDesc X,
+                      const double *ghost, long long ldg, MvDesc Y, double alpha, double beta) {
+  const int npairs = (n_local + 1) / 2;
+  if (npairs <= 0) return;
+  if (max_keys <= 8)
+    spmm_pair_cols<8>(s, npairs, rowptr, pptr, pkey, pmeta, vals, X, n_local, ghost, ldg, Y, alpha, beta);
+  else if (max_keys <= 12)
+    spmm_pair_cols<12>(s, npairs, rowptr, pptr, pkey, pmeta, vals, X, n_local, ghost, ldg, Y, alpha, beta);
+  else
+    throw Error(MIGMRES_EINVAL, "spmm_pair: more than 12 keys per row pair");
+}
+
+// -------------------------------------------------------------------------------------
 // C = A^T B (A: nrows x L, B: nrows x kb <= 16) on v_mfma_f64_16x16x4_f64.
 // MFMA M = 16 columns of A (one column tile), N = 16 columns of B, K = rows.
 // The K index of an MFMA may map to ANY row as long as A and B agree, so each lane loads

@@ -185,4 +185,61 @@ void galeri_rows(const std::string &kind, int nx, int ny, int nz, long long firs
   }
 }
 
+bool make_pair_plan(int n_local, const long long *rowptr, const int *xcols, PairPlan &out) {
+  const int P = (n_local + 1) / 2;
+  out.ptr.assign((size_t)P + 1, 0);
+  out.key.clear();
+  out.meta.clear();
+  out.key.reserve((size_t)(rowptr[n_local] / 2 + 8));
+  out.meta.reserve((size_t)(rowptr[n_local] / 2 + 8));
+  auto key_of = [&](int c) { return c < n_local ? (c >> 1) : -(1 + ((c - n_local) >> 1)); };
+  auto half_of = [&](int c) { return c < n_local ? (c & 1) : ((c - n_local) & 1); };
+  // ascending X-space order maps to: owned keys ascending, then ghost keys descending in value
+  auto rank_of = [&](int c) { return c < n_local ? (long long)(c >> 1) : (1LL << 40) + ((c - n_local) >> 1); };
+  for (int p = 0; p < P; ++p) {
+    const int rows[2] = {2 * p, 2 * p + 1};
+    long long b[2], e[2];
+    for (int h = 0; h < 2; ++h) {
+      if (rows[h] < n_local) {
+        b[h] = rowptr[rows[h]];
+        e[h] = rowptr[rows[h] + 1];
+      } else {
+        b[h] = e[h] = 0;
+      }
+      if (e[h] - b[h] > kPairMaxRow) return false;
+    }
+    long long i0 = b[0], i1 = b[1];
+    int nk = 0;
+    while (i0 < e[0] || i1 < e[1]) {
+      const long long r0 = i0 < e[0] ? rank_of(xcols[i0]) : (1LL << 62);
+      const long long r1 = i1 < e[1] ? rank_of(xcols[i1]) : (1LL << 62);
+      const long long r = r0 < r1 ? r0 : r1;
+      const int key = key_of(r == r0 ? xcols[i0] : xcols[i1]);
+      unsigned short m = 0xFFFF;
+      long long *it[2] = {&i0, &i1};
+      for (int h = 0; h < 2; ++h) {
+        // at most two entries of a row share a key (low half first in ascending order)
+        while (*it[h] < e[h] && rank_of(xcols[*it[h]]) == r) {
+          const int hf = half_of(xcols[*it[h]]);
+          const int shift = 4 * (2 * h + hf);
+          if (((m >> shift) & 0xF) != 0xF) return false;  // repeated column
+          m = (unsigned short)((m & ~(0xF << shift)) | ((int)(*it[h] - b[h]) << shift));
+          ++*it[h];
+        }
+      }
+      out.key.push_back(key);
+      out.meta.push_back(m);
+      if (++nk > kPairMaxKeys) return false;
+    }
+    if (nk > out.max_keys) out.max_keys = nk;
+    out.ptr[(size_t)p + 1] = (int)out.key.size();
+  }
+  // padding so the kernel's clamped reads of kPairMaxKeys slots stay in bounds
+  for (int i = 0; i < kPairMaxKeys; ++i) {
+    out.key.push_back(0);
+    out.meta.push_back(0xFFFF);
+  }
+  return true;
+}
+
 }  // namespace migmres

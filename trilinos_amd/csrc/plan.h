@@ -29,6 +29,22 @@ void local_crs(int n_local, const long long *rowptr, const long long *gcols, con
                const long long *colmap, int n_cols, long long first, int *lcols_out,
                double *vals_out);
 
+// Row-pair gather plan for k_spmm_pair (kernels.hip).  Rows (2p, 2p+1) share 16-byte
+// loads of aligned X pairs: for every row pair the sorted distinct pair keys of both rows'
+// X-space columns (owned column c -> c >> 1; ghost column n_local + g -> -(1 + (g >> 1))),
+// and per key a 16-bit map of which entry of each row reads its low / high half
+// (nibbles: row 0 low, row 0 high, row 1 low, row 1 high; 15 = none).  Each row's entries
+// stay in stored (ascending X-space) order, so the kernel's sums are the reference's.
+// Returns false (no plan) if a row has more than kPairMaxRow entries, a pair needs more
+// than kPairMaxKeys keys, or a row repeats a column.
+constexpr int kPairMaxRow = 8, kPairMaxKeys = 12;
+struct PairPlan {
+  std::vector<int> ptr, key;
+  std::vector<unsigned short> meta;
+  int max_keys = 0;  // largest key count of any pair (the kernel is instantiated for <= 8 and <= 12)
+};
+bool make_pair_plan(int n_local, const long long *rowptr, const int *xcols, PairPlan &out);
+
 void galeri_rows(const std::string &kind, int nx, int ny, int nz, long long first, int n_local,
                  std::vector<long long> &rowptr, std::vector<long long> &gcols,
                  std::vector<double> &vals);

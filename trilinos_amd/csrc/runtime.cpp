@@ -2,6 +2,7 @@
 #include "runtime.h"
 
 #include <chrono>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <string>
@@ -60,7 +61,7 @@ void migmres_ctx::allreduce(double *d, size_t n, bool max) {
 
 const char *kKernelClassNames[K_NUM_CLASSES] = {"spmm", "gemm_tn", "reduce", "gemm_nn", "coldot",
                                                 "axpby", "scale", "fill", "copy", "random", "pack",
-                                                "findbasis", "gemm_nn_dot"};
+                                                "findbasis", "gemm_nn_dot", "nn_tn"};
 
 hipEvent_t migmres_ctx::get_event() {
   if (!event_pool.empty()) {
@@ -502,7 +503,7 @@ void mv_assign(const migmres_mv &A, migmres_mv &Y) {
 // ------------------------------------------------------------------------------------
 migmres_crs::~migmres_crs() {
   for (void *p : {(void *)d_rowptr, (void *)d_cols, (void *)d_export, (void *)d_vals,
-                  (void *)d_send, (void *)d_ghost})
+                  (void *)d_send, (void *)d_ghost, (void *)d_pptr, (void *)d_pkey, (void *)d_pmeta})
     if (p) hipFree(p);
 }
 
@@ -599,11 +600,27 @@ migmres_crs *crs_create(migmres_ctx *ctx, long long n_global, long long first, i
     for (int r = 0; r <= n_local; ++r) rp32[(size_t)r] = (int)rowptr[r];
     MIG_HIP(hipMalloc(&A->d_rowptr, sizeof(int) * (n_local + 1)));
     MIG_HIP(hipMalloc(&A->d_cols, sizeof(int) * (nnz > 0 ? nnz : 1)));
-    MIG_HIP(hipMalloc(&A->d_vals, sizeof(double) * (nnz > 0 ? nnz : 1)));
+    MIG_HIP(hipMalloc(&A->d_vals, sizeof(double) * (nnz + 8)));
+    MIG_HIP(hipMemset(A->d_vals, 0, sizeof(double) * (nnz + 8)));
     MIG_HIP(hipMemcpy(A->d_rowptr, rp32.data(), sizeof(int) * (n_local + 1), hipMemcpyHostToDevice));
     if (nnz) {
       MIG_HIP(hipMemcpy(A->d_cols, lcols.data(), sizeof(int) * nnz, hipMemcpyHostToDevice));
       MIG_HIP(hipMemcpy(A->d_vals, lvals.data(), sizeof(double) * nnz, hipMemcpyHostToDevice));
+    }
+    {
+      PairPlan pp;
+      const char *np = std::getenv("MIGMRES_NO_PAIR_SPMM");
+      if (!(np && np[0] == '1') && make_pair_plan(n_local, rowptr, lcols.data(), pp)) {
+        MIG_HIP(hipMalloc(&A->d_pptr, sizeof(int) * pp.ptr.size()));
+        MIG_HIP(hipMalloc(&A->d_pkey, sizeof(int) * pp.key.size()));
+        MIG_HIP(hipMalloc(&A->d_pmeta, sizeof(unsigned short) * pp.meta.size()));
+        MIG_HIP(hipMemcpy(A->d_pptr, pp.ptr.data(), sizeof(int) * pp.ptr.size(), hipMemcpyHostToDevice));
+        MIG_HIP(hipMemcpy(A->d_pkey, pp.key.data(), sizeof(int) * pp.key.size(), hipMemcpyHostToDevice));
+        MIG_HIP(hipMemcpy(A->d_pmeta, pp.meta.data(), sizeof(unsigned short) * pp.meta.size(),
+                          hipMemcpyHostToDevice));
+        A->use_pairs = true;
+        A->pair_max_keys = pp.max_keys;
+      }
     }
     if (!A->export_lids.empty()) {
       MIG_HIP(hipMalloc(&A->d_export, sizeof(int) * A->export_lids.size()));
@@ -630,7 +647,9 @@ void crs_apply(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, double alpha,
       if (A.d_ghost) hipFree(A.d_ghost);
       A.d_send = A.d_ghost = nullptr;
       MIG_HIP(hipMalloc(&A.d_send, sizeof(double) * ((size_t)n_export * k + 1)));
-      MIG_HIP(hipMalloc(&A.d_ghost, sizeof(double) * ((size_t)n_remote * k + 1)));
+      A.ldg = (n_remote + 1) & ~1LL;
+      MIG_HIP(hipMalloc(&A.d_ghost, sizeof(double) * ((size_t)A.ldg * k + 2)));
+      MIG_HIP(hipMemset(A.d_ghost, 0, sizeof(double) * ((size_t)A.ldg * k + 2)));
       A.halo_k = k;
     }
     auto t0 = std::chrono::steady_clock::now();
@@ -642,14 +661,18 @@ void crs_apply(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, double alpha,
                           c->comm, c->stream));
     for (auto &nb : A.recv_nbrs)
       for (int col = 0; col < k; ++col)
-        MIG_NCCL(ncclRecv(A.d_ghost + (size_t)col * n_remote + nb.offset, nb.count, ncclDouble, nb.pid,
+        MIG_NCCL(ncclRecv(A.d_ghost + (size_t)col * A.ldg + nb.offset, nb.count, ncclDouble, nb.pid,
                           c->comm, c->stream));
     MIG_NCCL(ncclGroupEnd());
     c->comm_seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
   ProfScope ps(c, K_SPMM, 12.0 * A.nnz + 4.0 * (A.n_local + 1) + 8.0 * A.n_local * k * (beta == 0.0 ? 2.0 : 3.0));
-  launch_spmm(c->stream, 0, A.n_local, A.d_rowptr, A.d_cols, A.d_vals, X.desc(), A.n_local,
-              A.d_ghost, n_remote, Y.desc(), alpha, beta);
+  if (A.use_pairs)
+    launch_spmm_pair(c->stream, A.n_local, A.pair_max_keys, A.d_rowptr, A.d_pptr, A.d_pkey, A.d_pmeta, A.d_vals, X.desc(),
+                     A.d_ghost, A.ldg, Y.desc(), alpha, beta);
+  else
+    launch_spmm(c->stream, 0, A.n_local, A.d_rowptr, A.d_cols, A.d_vals, X.desc(), A.n_local, A.d_ghost,
+                A.ldg, Y.desc(), alpha, beta);
 }
 
 }  // namespace migmres
@@ -697,6 +720,20 @@ extern "C" int migmres_plan_local_crs(long long first, int n_local, const long l
                                       double *vals_out) {
   return guard([&] {
     local_crs(n_local, rowptr, gcols, vals, colmap, n_cols, first, lcols_out, vals_out);
+  });
+}
+
+extern "C" int migmres_plan_pairs(int n_local, const long long *rowptr, const int *xcols, int *ptr_out,
+                                  int *key_out, unsigned short *meta_out, long long *nkeys, int *ok) {
+  return guard([&] {
+    MIG_CHECK(n_local >= 0 && rowptr && nkeys && ok, "plan_pairs: bad arguments");
+    PairPlan pp;
+    *ok = make_pair_plan(n_local, rowptr, xcols, pp) ? 1 : 0;
+    *nkeys = *ok ? (long long)pp.key.size() : 0;
+    if (!*ok) return;
+    if (ptr_out) std::memcpy(ptr_out, pp.ptr.data(), sizeof(int) * pp.ptr.size());
+    if (key_out) std::memcpy(key_out, pp.key.data(), sizeof(int) * pp.key.size());
+    if (meta_out) std::memcpy(meta_out, pp.meta.data(), sizeof(unsigned short) * pp.meta.size());
   });
 }
 

@@ -12,7 +12,7 @@
 
 // Per-kernel-class profiling with HIP events on the context stream (bench.py roofline).
 enum KernelClass { K_SPMM = 0, K_GEMM_TN, K_REDUCE, K_GEMM_NN, K_COLDOT, K_AXPBY, K_SCALE, K_FILL,
-                   K_COPY, K_RANDOM, K_PACK, K_FB, K_GEMM_NN_DOT, K_NUM_CLASSES };
+                   K_COPY, K_RANDOM, K_PACK, K_FB, K_GEMM_NN_DOT, K_NN_TN, K_NUM_CLASSES };
 extern const char *kKernelClassNames[K_NUM_CLASSES];
 
 struct migmres_ctx;
@@ -101,8 +101,14 @@ struct migmres_crs {
   };
   std::vector<Nbr> recv_nbrs, send_nbrs;
   int *d_rowptr = nullptr, *d_cols = nullptr, *d_export = nullptr;
-  double *d_vals = nullptr;
+  double *d_vals = nullptr;  // padded by 8 zero entries (row-pair kernel reads 8 per row)
+  // row-pair gather plan (k_spmm_pair); null when the matrix does not fit it
+  int *d_pptr = nullptr, *d_pkey = nullptr;
+  unsigned short *d_pmeta = nullptr;
+  bool use_pairs = false;
+  int pair_max_keys = 0;
   double *d_send = nullptr, *d_ghost = nullptr;
+  long long ldg = 0;  // ghost block leading dimension: n_remote rounded up to even, padding zero
   int halo_k = 0;
   ~migmres_crs();
 };

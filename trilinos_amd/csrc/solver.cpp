@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <map>
@@ -258,6 +259,8 @@ struct FastIcgs {
   double *h = nullptr;  // pinned: state + C
   MvPtr tmpX;
   long long calls = 0, fallbacks = 0;
+  bool use_fused = true;  // MIGMRES_NO_FUSED_NN_TN=1 selects the two-kernel form (A/B timing)
+  int nt_cache[257] = {};
 
   ~FastIcgs() { release(); }
   void release() {
@@ -283,7 +286,11 @@ struct FastIcgs {
     Lmax = lmax;
     nblk_tn = gemm_tn_blocks(nl);
     nblk_ic = icgs_blocks(nl);
-    const size_t np = std::max((size_t)nblk_tn * 512 * 16, (size_t)nblk_ic * 17);
+    for (int &v : nt_cache) v = 0;
+    const char *nf = std::getenv("MIGMRES_NO_FUSED_NN_TN");
+    use_fused = !(nf && nf[0] == '1');
+    const size_t np = std::max({(size_t)nblk_tn * 512 * 16, (size_t)nblk_ic * 17,
+                                (size_t)nn_tn_blocks(nl, 16) * 256 * 16});
     MIG_HIP(hipMalloc(&partial, sizeof(double) * np));
     MIG_HIP(hipMalloc(&R1, sizeof(double) * (size_t)(lmax + k) * k));
     MIG_HIP(hipMalloc(&R2, sizeof(double) * (size_t)(lmax + k) * k));
@@ -336,6 +343,34 @@ struct FastIcgs {
     }
     ProfScope ps(ctx, K_GEMM_NN_DOT, 8.0 * n_local * (L + 2.0 * k));
     launch_gemm_nn_dot(ctx->stream, Q, L, M, ldm, X, n_local, -1.0, 1.0, 1, X, partial, nblk_ic);
+  }
+
+  // X = X - Q C1 (C1 leading dim ldc1) then out = Q^T X, summed over ranks: one fused pass
+  // over Q when the shape allows it, else MvTimesMatAddMv followed by MvTransMv.
+  void nn_then_tn(const MvDesc &Q, int L, const double *C1, int ldc1, const MvDesc &X, int k, double *out) {
+    // Measured at 256^3, k = 8 (tools/mb_lib.cpp): the fused kernel is fp64-MFMA bound and
+    // wins over the two streaming kernels only for 32 <= L <= 64 and L >= 160.
+    const bool fused_wins = (L >= 32 && L <= 64) || L >= 160;
+    if (use_fused && fused_wins && !Q.cols && nn_tn_supported(L, k)) {
+      const int nb = nt_blocks(L);
+      {
+        ProfScope ps(ctx, K_NN_TN, 8.0 * n_local * (L + 2.0 * k) + 8.0 * nb * L * k);
+        launch_nn_tn(ctx->stream, Q, L, C1, ldc1, X, n_local, partial, nb);
+      }
+      {
+        ProfScope ps(ctx, K_REDUCE, 8.0 * nb * L * k);
+        launch_reduce_partials_ld(ctx->stream, partial, nb, L, k, L, 1.0, out);
+      }
+      allreduce(out, (size_t)L * k);
+      return;
+    }
+    nn(Q, L, C1, ldc1, X, k, false);
+    tn(Q, L, X, k, out, L);
+  }
+
+  int nt_blocks(int L) {
+    if (nt_cache[L] == 0) nt_cache[L] = nn_tn_blocks(n_local, L);
+    return nt_cache[L];
   }
 
   void find_basis(const MvDesc &X, int k, int complete) {
@@ -393,8 +428,7 @@ struct FastIcgs {
     const MvDesc xd = X.desc(), qd = Q.desc();
     if (k == 1) {  // blkOrtho1, then MvDot and MvScale
       tn(qd, L, xd, 1, R1, L);
-      nn(qd, L, R1, L, xd, 1, false);
-      tn(qd, L, xd, 1, R2, L);
+      nn_then_tn(qd, L, R1, L, xd, 1, R2);
       nn(qd, L, R2, L, xd, 1, true);
       reduce_small(1);
       launch_fb_scalar(ctx->stream, st, red, 4, 0, 1, 0);
@@ -421,8 +455,7 @@ struct FastIcgs {
       allreduce(R1, (size_t)(L + k) * k);
     }
     launch_blk_old(ctx->stream, st, R1, L + k, L, k);
-    nn(qd, L, R1, L + k, xd, k, false);
-    tn(qd, L, xd, k, R2, L);
+    nn_then_tn(qd, L, R1, L + k, xd, k, R2);
     nn(qd, L, R2, L, xd, k, true);
     reduce_small(k);
     launch_fb_scalar(ctx->stream, st, red, 3, 0, k, 0);
