@@ -50,12 +50,14 @@ double timeit(F f, int reps = 10) {
 int main(int argc, char **argv) {
   const int m = argc > 1 ? atoi(argv[1]) : 256;
   const long long n = (long long)m * m * m;
-  const long long ld = (n + 63) / 64 * 64;
+  const long long ld = (n + 63) / 64 * 64 + (argc > 2 ? atoi(argv[2]) : 0);
   const int k = 8, Lmax = 216;
   double *V, *P, *R, *S;
   CK(hipMalloc(&V, sizeof(double) * ld * Lmax + 256));
   CK(hipMalloc(&P, sizeof(double) * 4096 * 512 * 16 + sizeof(double) * 2048 * 256 * 16));
   CK(hipMalloc(&R, sizeof(double) * 512 * 16));
+  double *SINK;
+  CK(hipMalloc(&SINK, sizeof(double) * 256 * 4096));
   CK(hipMalloc(&S, sizeof(double) * ld));
   fill<<<(ld * Lmax + 255) / 256, 256>>>(V, ld * Lmax, 1);
   CK(hipMemset(R, 0, sizeof(double) * 512 * 16));
@@ -74,8 +76,8 @@ int main(int argc, char **argv) {
     const int nb2 = icgs_blocks((int)n);
     double t_nnd = timeit([&] { launch_gemm_nn_dot(s, Q, L, R, L + k, X, (int)n, -1.0, 1.0, 1, X, P, nb2); });
     const double by_nn = 8.0 * n * (L + 2 * k);
-    const int nbf = nn_tn_blocks((int)n, L);
-    double t_f = timeit([&] { launch_nn_tn(s, Q, L, R, L + k, X, (int)n, P, nbf); });
+    const int nbf = nn_tn_blocks((int)n, L, k);
+    double t_f = timeit([&] { launch_nn_tn(s, Q, L, R, L + k, X, (int)n, P, nbf, SINK); });
     printf("L=%3d  tn %7.3f ms %6.0f GB/s | reduce %6.1f us | nn %7.3f ms %6.0f GB/s | nn_dot %7.3f ms %6.0f GB/s"
            " | nn_tn %7.3f ms %6.0f GB/s (%d wg)\n", L,
            t_tn, by_tn / t_tn / 1e6, t_red * 1e3, t_nn, by_nn / t_nn / 1e6, t_nnd, by_nn / t_nnd / 1e6, t_f,
@@ -97,8 +99,8 @@ int main(int argc, char **argv) {
     launch_gemm_nn(s, Q, L, R, L + k, X, (int)n, -1.0, 1.0);
     launch_gemm_tn_partial(s, Q, L, X, k, (int)n, P, nblk);
     launch_reduce_partials_ld(s, P, nblk, L, k, L, 1.0, R2a);
-    const int nbf = nn_tn_blocks((int)n, L);
-    launch_nn_tn(s, Q, L, R, L + k, XB, (int)n, P, nbf);
+    const int nbf = nn_tn_blocks((int)n, L, k);
+    launch_nn_tn(s, Q, L, R, L + k, XB, (int)n, P, nbf, SINK);
     launch_reduce_partials_ld(s, P, nbf, L, k, L, 1.0, R2b);
     CK(hipDeviceSynchronize());
     std::vector<double> xa((size_t)ld * k), xb((size_t)ld * k), ra(L * k), rb(L * k);
@@ -120,8 +122,9 @@ int main(int argc, char **argv) {
   CK(hipMalloc(&st, sizeof(IcgsState)));
   CK(hipMemset(st, 0, sizeof(IcgsState)));
   MvDesc X{V, ld, nullptr, k};
-  const int nb2 = icgs_blocks((int)n);
-  for (int j : {0, 1, 3, 7}) {
+  for (int nb2 : {icgs_blocks((int)n), 1024, 2048, 4096})
+  for (int j : {1, 3, 7}) {
+    printf("nb=%d ", nb2);
     double ta = timeit([&] { launch_fb_a(s, X, j, st, (int)n, P, nb2); });
     double tb = j ? timeit([&] { launch_fb_b(s, X, j, st, S, (int)n, P, nb2); }) : 0;
     double tc = j ? timeit([&] { launch_fb_c(s, X, j, st, S, (int)n, P, nb2); }) : 0;

@@ -22,14 +22,21 @@ void launch_gemm_nn_dot(hipStream_t s, MvDesc A, int L, const double *M, int ldm
                         int nrows, double alpha, double beta, int dmode, MvDesc D, double *partial,
                         int nblocks);
 // X1 = X - Q C1 in place and per-workgroup partials of Q^T X1 (L x k, column-major).
+// sink: scratch of nblocks * 256 doubles that absorbs the stores of padding lanes.
 bool nn_tn_supported(int L, int k);
-int nn_tn_blocks(int nrows, int L);
+int nn_tn_blocks(int nrows, int L, int k);
 void launch_nn_tn(hipStream_t s, MvDesc Q, int L, const double *C1, int ldc, MvDesc X, int nrows,
-                  double *partial, int nblocks);
+                  double *partial, int nblocks, double *sink);
 void launch_fb_a(hipStream_t s, MvDesc X, int j, const IcgsState *st, int nrows, double *partial, int nb);
 void launch_fb_b(hipStream_t s, MvDesc X, int j, const IcgsState *st, double *S, int nrows, double *partial, int nb);
 void launch_fb_c(hipStream_t s, MvDesc X, int j, const IcgsState *st, const double *S, int nrows, double *partial,
                  int nb);
+// Two-pass-per-column findBasis (see icgs.hip): a01 head, b2 = normalise previous column +
+// first update + second projection, ca = second update + next column's first projection.
+void launch_fb_a01(hipStream_t s, MvDesc X, int nrows, double *partial, int nb);
+void launch_fb_b2(hipStream_t s, MvDesc X, int j, const IcgsState *st, double *S, int nrows, double *partial, int nb);
+void launch_fb_ca(hipStream_t s, MvDesc X, int j, int has_next, const IcgsState *st, const double *S, int nrows,
+                  double *partial, int nb);
 void launch_scale_col(hipStream_t s, MvDesc X, int j, const IcgsState *st, int nrows);
 void launch_fb_scalar(hipStream_t s, IcgsState *st, const double *red, int stage, int j, int k, int complete);
 void launch_blk_old(hipStream_t s, IcgsState *st, const double *G, int ldg, int L, int k);

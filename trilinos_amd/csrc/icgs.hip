@@ -52,9 +52,11 @@ __device__ __forceinline__ void block_reduce_store(double (&v)[NV], int nv, doub
   }
 }
 
+// 1024 workgroups (4 per CU) stream the findBasis columns at 5.3-5.6 TB/s where 512 gave
+// 3.8-4.4 TB/s (tools/mb_lib.cpp, 256^3).
 int icgs_blocks(int nrows) {
-  const int b = cdiv_(nrows, 4096);
-  return b < 1 ? 1 : (b > 512 ? 512 : b);
+  const int b = cdiv_(nrows, 2048);
+  return b < 1 ? 1 : (b > 1024 ? 1024 : b);
 }
 
 // out[o] = sum_b partial[b * nv + o], o < nv <= 17: one workgroup, every thread sums a
@@ -184,21 +186,28 @@ void launch_gemm_nn_dot(hipStream_t s, MvDesc A, int L, const double *M, int ldm
 //   X1 = X - Q C1 (in place)   and   partial[wg] = Q^T X1  (L x k per workgroup)
 // One pass over Q instead of two (the reference does MvTimesMatAddMv, then MvTransMv).
 // A workgroup stages a 16-row chunk of Q (all L <= 256 columns) in LDS, then
-//   phase 1: D = Qc C1 on MFMA (M = the 16 rows, K = Q columns split over the 4 waves,
-//            N = X columns; C1 register resident), waves summed in a fixed order -> X1,
-//   phase 2: acc += Qc^T X1 on MFMA (M = 16 Q columns per tile, K = the 16 rows),
+//   phase 1: D = Qc C1 (16 rows x k, K = Q columns split over the 4 waves, C1 register
+//            resident), waves summed in a fixed order -> X1 (written out, kept in LDS),
+//   phase 2: acc += Qc^T X1 (L x k over the chunk's 16 rows),
 // while the loads of the next two chunks are in flight in registers (counted waits: the
 // loads are branch-free and the barriers are raw s_barrier, see lds_barrier()).
-// MFMA rather than VALU: the VALU form needs every lane to read whole C1 / X1 rows from
-// LDS (broadcast reads), which made it LDS-bound; here each lane reads one f64 per MFMA.
-// LDS: Qs[Lp][17] (odd stride: both phases' reads are conflict-free), Xs[16][16], red[3][4][64].
+// Both products use v_mfma_f64_4x4x4f64 (4 independent 4x4x4 blocks per instruction):
+// measured 72 TF/s against 47 TF/s for v_mfma_f64_16x16x4f64 (tools/mb_mfma.hip), and its
+// 4-wide N matches k = 4, 8, 12, 16 without padding.  Lane maps (probed on gfx950):
+//   A: lane 16k + 4b + m -> block b row m, K index k;  B: lane 16k + 4b + n -> block b
+//   column n;  D: lane 16m + 4b + n -> block b (m, n).
+// With lane l, c = l & 15, g = l >> 4 the A operand is element (c, g) of a 16 x 4 tile
+// (rows 4b + m = c), the same addressing as a 16x16x4 A operand.
+// LDS: Qs[Lp][17] (odd stride: both phases' reads are conflict-free), Xs[16][16], red[4][4][64].
 // -------------------------------------------------------------------------------------
-typedef double d4_ __attribute__((ext_vector_type(4)));
 constexpr int NT_ROWS = 16, NT_MAXL = 256, NT_LDQ = 17;
+#ifndef NT_DIAG_MASK  // bit 0 phase 1, bit 1 phase 2, bit 2 LDS staging (tools/mb_nntn.hip)
+#define NT_DIAG_MASK 7
+#endif
 
 static size_t nt_lds_bytes(int L) {
   const int Lp = (L + 15) & ~15;
-  return sizeof(double) * ((size_t)Lp * NT_LDQ + 256 + 3 * 256);
+  return sizeof(double) * ((size_t)Lp * NT_LDQ + 256 + 4 * 256);
 }
 
 // Workgroup barrier for LDS hand-offs only.  __syncthreads()'s release fence waits for
@@ -210,27 +219,40 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int NM>
+__device__ __forceinline__ double mfma4(double a, double b, double c) {
+  return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
+}
+
+template <int NM, int NJ>
 __global__ __launch_bounds__(256, 2) void k_nn_tn(MvDesc Q, int L, const double *__restrict__ C1, int ldc,
-                                                  MvDesc X, int k, int nrows, double *__restrict__ partial) {
+                                                  MvDesc X, int k, int nrows, double *__restrict__ partial,
+                                                  double *__restrict__ sink) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int Lp = (L + 15) & ~15;
   double *Qs = sm;
   double *Xs = sm + (size_t)Lp * NT_LDQ;
   double *red = Xs + 256;
   const int t = threadIdx.x, w = t >> 6, l = t & 63, c = l & 15, g = l >> 4;
+  const int n4 = l & 3;                            // B / D column within a 4-wide group
+  const int drow = 4 * ((l >> 2) & 3) + (l >> 4);  // D row of this lane (block b, row m)
   for (int e = t; e < (Lp - L) * NT_LDQ; e += 256) Qs[L * NT_LDQ + e] = 0.0;
 
-  // phase-1 B operand: C1[i = 4s + g][j = c] for the wave's K steps s = w + 4m
-  double b1[16];
+  // phase-1 B operand: C1[i = 4s + g][j = 4 jg + n4] for the wave's K steps s = w + 4m
+  double b1[16][NJ];
 #pragma unroll
   for (int m = 0; m < 16; ++m) {
     const int i = 4 * (w + 4 * m) + g;
-    b1[m] = (i < L && c < k) ? C1[i + (long long)c * ldc] : 0.0;
-  }
-  d4_ acc2[4];
 #pragma unroll
-  for (int m = 0; m < 4; ++m) acc2[m] = d4_{0.0, 0.0, 0.0, 0.0};
+    for (int jg = 0; jg < NJ; ++jg) {
+      const int j = 4 * jg + n4;
+      b1[m][jg] = (i < L && j < k) ? C1[i + (long long)j * ldc] : 0.0;
+    }
+  }
+  double acc2[4][NJ];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int jg = 0; jg < NJ; ++jg) acc2[m][jg] = 0.0;
 
   // loader: Q column lcol + 32 m (clamped to L - 1: duplicates rewrite the same value),
   // rows lrow, lrow + 1 -- 8 lanes = one 128-B line.  Q is a contiguous column range.
@@ -243,9 +265,13 @@ __global__ __launch_bounds__(256, 2) void k_nn_tn(MvDesc Q, int L, const double 
     scol[m] = i < L ? i : L - 1;
     qcol[m] = Q.base + (long long)scol[m] * Q.ld + lrow;
   }
-  // wave 0 lane (g, c) updates X1[g + 4q][c], q < 4
-  const bool xl = c < k;
-  double *xcol = colp_(X, xl ? c : k - 1);
+  // X1 rows: wave w updates rows 4w + (l >> 4), column l & 15 of every chunk (one 8-byte
+  // load and one store per lane and chunk, the same in every wave so that the wait counts
+  // stay static; columns >= k read column k - 1 and store into the sink).
+  const int xrow = 4 * w + (l >> 4), xc = l & 15;
+  const bool xcol_ok = xc < k;
+  const double *xsrc = colp_(X, xcol_ok ? xc : k - 1);
+  double *xdst = colp_(X, xcol_ok ? xc : k - 1);
   const long long nchunks = (nrows + NT_ROWS - 1) / NT_ROWS;
   const long long G = gridDim.x;
   auto clampc = [&](long long chunk) { return chunk < nchunks ? chunk : nchunks - 1; };
@@ -254,114 +280,131 @@ __global__ __launch_bounds__(256, 2) void k_nn_tn(MvDesc Q, int L, const double 
 #pragma unroll
     for (int m = 0; m < NM; ++m) p[m] = *(const d2 *)(qcol[m] + chunk * NT_ROWS);
   };
-  auto loadx = [&](double(&xv)[4], long long chunk) {
-    chunk = clampc(chunk);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) xv[q] = xcol[chunk * NT_ROWS + g + 4 * q];
-  };
+  auto loadx = [&](double &xv, long long chunk) { xv = xsrc[clampc(chunk) * NT_ROWS + xrow]; };
 
   // A chunk past the end (second half of the last 2-chunk step) runs the same instruction
   // stream on clamped data with X1 = 0, adding nothing; keeping both halves unconditional
   // keeps the wait counts static.
-  auto body = [&](d2(&p)[NM], double(&xv)[4], long long chunk) {
+  auto body = [&](d2(&p)[NM], double &xv, long long chunk) {
     const bool live = chunk < nchunks;
     const long long r0 = chunk * NT_ROWS;
 #pragma unroll
     for (int m = 0; m < NM; ++m) {
-      Qs[scol[m] * NT_LDQ + lrow] = p[m].x;
-      Qs[scol[m] * NT_LDQ + lrow + 1] = p[m].y;
+      if (NT_DIAG_MASK & 4) {
+        Qs[scol[m] * NT_LDQ + lrow] = p[m].x;
+        Qs[scol[m] * NT_LDQ + lrow + 1] = p[m].y;
+      } else if (p[m].x == 12345.0) {
+        Qs[0] = p[m].y;
+      }
     }
     lds_barrier();
     loadq(p, chunk + 2 * G);
-    // phase 1: this wave's share of D[r][j] = sum_i Q[r][i] C1[i][j], two MFMA chains
-    d4_ a1 = d4_{0.0, 0.0, 0.0, 0.0}, a2 = d4_{0.0, 0.0, 0.0, 0.0};
+    // phase 1: this wave's share of D[r][j] = sum_i Q[r][i] C1[i][j]
+    double a1[NJ];
 #pragma unroll
-    for (int m = 0; m < 16; m += 2) {
-      const int s0 = w + 4 * m, s1 = w + 4 * (m + 1);
-      if (4 * s0 < L) a1 = __builtin_amdgcn_mfma_f64_16x16x4f64(Qs[(4 * s0 + g) * NT_LDQ + c], b1[m], a1, 0, 0, 0);
-      if (4 * s1 < L) a2 = __builtin_amdgcn_mfma_f64_16x16x4f64(Qs[(4 * s1 + g) * NT_LDQ + c], b1[m + 1], a2, 0, 0, 0);
-    }
-    a1 += a2;
-    if (w > 0) {
+    for (int jg = 0; jg < NJ; ++jg) a1[jg] = 0.0;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) red[((w - 1) * 4 + q) * 64 + l] = a1[q];
-    }
-    lds_barrier();
-    if (w == 0) {
+    for (int m = 0; m < ((NT_DIAG_MASK & 1) ? 16 : 0); ++m) {
+      const int s = w + 4 * m;
+      if (4 * s < L) {
+        const double qa = Qs[(4 * s + g) * NT_LDQ + c];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int r = g + 4 * q;
-        const double d = (a1[q] + red[q * 64 + l]) + (red[(4 + q) * 64 + l] + red[(8 + q) * 64 + l]);
-        const double x1 = (xl && live) ? xv[q] - d : 0.0;
-        if (xl && live && r0 + r < nrows) xcol[r0 + r] = x1;
-        Xs[r * 16 + c] = x1;
+        for (int jg = 0; jg < NJ; ++jg) a1[jg] = mfma4(qa, b1[m][jg], a1[jg]);
       }
+    }
+#pragma unroll
+    for (int jg = 0; jg < NJ; ++jg) red[(w * 4 + jg) * 64 + l] = a1[jg];
+    lds_barrier();
+    {
+      // wave w: rows 4w + (l >> 4); D lane of (row, column) = 16 (l >> 4) + 4 w + (column & 3)
+      const int jg = (xc >> 2) < NJ ? (xc >> 2) : NJ - 1;
+      const int o = 16 * (l >> 4) + 4 * w + (xc & 3);
+      const double d = (red[jg * 64 + o] + red[(4 + jg) * 64 + o]) +
+                       (red[(8 + jg) * 64 + o] + red[(12 + jg) * 64 + o]);
+      const bool ok = xcol_ok && live && r0 + xrow < nrows;
+      const double x1 = ok ? xv - d : 0.0;
+      double *dst = ok ? xdst + r0 + xrow : sink + (blockIdx.x * 256 + t);
+      *dst = x1;
+      Xs[xrow * 16 + xc] = x1;
       loadx(xv, chunk + 2 * G);
     }
     lds_barrier();
-    // phase 2: acc[tile] += Q[:, tile]^T X1 over the chunk's 16 rows
-    double xb[4];
+    // phase 2: acc[tile][jg] += Q[:, tile]^T X1[:, 4 jg .. 4 jg + 3] over the 16 rows
+    double xb[4][NJ];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) xb[s] = Xs[(4 * s + g) * 16 + c];
+    for (int s = 0; s < 4; ++s)
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
+      for (int jg = 0; jg < NJ; ++jg) xb[s][jg] = Xs[(4 * s + g) * 16 + 4 * jg + n4];
+#pragma unroll
+    for (int m = 0; m < ((NT_DIAG_MASK & 2) ? 4 : 0); ++m) {
       const int tt = w + 4 * m;
       if (16 * tt < L) {
 #pragma unroll
-        for (int s = 0; s < 4; ++s)
-          acc2[m] = __builtin_amdgcn_mfma_f64_16x16x4f64(Qs[(16 * tt + c) * NT_LDQ + 4 * s + g], xb[s], acc2[m],
-                                                         0, 0, 0);
+        for (int s = 0; s < 4; ++s) {
+          const double qa = Qs[(16 * tt + c) * NT_LDQ + 4 * s + g];
+#pragma unroll
+          for (int jg = 0; jg < NJ; ++jg) acc2[m][jg] = mfma4(qa, xb[s][jg], acc2[m][jg]);
+        }
       }
     }
     lds_barrier();
   };
 
   d2 pa[NM], pb[NM];
-  double xa[4] = {0.0, 0.0, 0.0, 0.0}, xb2[4] = {0.0, 0.0, 0.0, 0.0};
+  double xa, xb2;
   const long long ch0 = blockIdx.x;
   loadq(pa, ch0);
-  if (w == 0) loadx(xa, ch0);
+  loadx(xa, ch0);
   asm volatile("" ::: "memory");  // keep pa's loads older than pb's (static wait counts in the loop)
   loadq(pb, ch0 + G);
-  if (w == 0) loadx(xb2, ch0 + G);
+  loadx(xb2, ch0 + G);
   for (long long ch = ch0; ch < nchunks; ch += 2 * G) {
     body(pa, xa, ch);
     body(pb, xb2, ch + G);
   }
-  if (c < k) {
-    double *out = partial + (long long)blockIdx.x * L * k;
+  double *out = partial + (long long)blockIdx.x * L * k;
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const int tt = w + 4 * m;
+  for (int m = 0; m < 4; ++m) {
+    const int tt = w + 4 * m;
+    const int i = 16 * tt + drow;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int i = 16 * tt + g + 4 * q;
-        if (i < L) out[i + (long long)c * L] = acc2[m][q];
-      }
+    for (int jg = 0; jg < NJ; ++jg) {
+      const int j = 4 * jg + n4;
+      if (i < L && j < k) out[i + (long long)j * L] = acc2[m][jg];
     }
   }
 }
 
-typedef void (*nt_kernel_t)(MvDesc, int, const double *, int, MvDesc, int, int, double *);
+typedef void (*nt_kernel_t)(MvDesc, int, const double *, int, MvDesc, int, int, double *, double *);
 
-static nt_kernel_t nt_pick(int L) {
+template <int NJ>
+static nt_kernel_t nt_pick_nm(int L) {
   switch ((L + 31) >> 5) {
-    case 1: return k_nn_tn<1>;
-    case 2: return k_nn_tn<2>;
-    case 3: return k_nn_tn<3>;
-    case 4: return k_nn_tn<4>;
-    case 5: return k_nn_tn<5>;
-    case 6: return k_nn_tn<6>;
-    case 7: return k_nn_tn<7>;
-    default: return k_nn_tn<8>;
+    case 1: return k_nn_tn<1, NJ>;
+    case 2: return k_nn_tn<2, NJ>;
+    case 3: return k_nn_tn<3, NJ>;
+    case 4: return k_nn_tn<4, NJ>;
+    case 5: return k_nn_tn<5, NJ>;
+    case 6: return k_nn_tn<6, NJ>;
+    case 7: return k_nn_tn<7, NJ>;
+    default: return k_nn_tn<8, NJ>;
   }
 }
 
-int nn_tn_blocks(int nrows, int L) {
+static nt_kernel_t nt_pick(int L, int k) {
+  switch ((k + 3) >> 2) {
+    case 1: return nt_pick_nm<1>(L);
+    case 2: return nt_pick_nm<2>(L);
+    case 3: return nt_pick_nm<3>(L);
+    default: return nt_pick_nm<4>(L);
+  }
+}
+
+int nn_tn_blocks(int nrows, int L, int k) {
   int per_cu = 0, dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nt_pick(L), 256, nt_lds_bytes(L)) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nt_pick(L, k), 256, nt_lds_bytes(L)) != hipSuccess ||
       per_cu < 1 || cus < 1) {
     per_cu = 2;
     cus = 256;
@@ -375,11 +418,12 @@ int nn_tn_blocks(int nrows, int L) {
 bool nn_tn_supported(int L, int k) { return L >= 1 && L <= NT_MAXL && k >= 1 && k <= 16; }
 
 void launch_nn_tn(hipStream_t s, MvDesc Q, int L, const double *C1, int ldc, MvDesc X, int nrows,
-                  double *partial, int nblocks) {
+                  double *partial, int nblocks, double *sink) {
   const int k = X.ncols;
   if (!nn_tn_supported(L, k)) throw Error(MIGMRES_EINVAL, "nn_tn: 1 <= L <= 256 and 1 <= k <= 16");
   if (Q.cols) throw Error(MIGMRES_EINVAL, "nn_tn: Q must be a contiguous column range");
-  hipLaunchKernelGGL(nt_pick(L), dim3(nblocks), dim3(256), nt_lds_bytes(L), s, Q, L, C1, ldc, X, k, nrows, partial);
+  hipLaunchKernelGGL(nt_pick(L, k), dim3(nblocks), dim3(256), nt_lds_bytes(L), s, Q, L, C1, ldc, X, k, nrows,
+                     partial, sink);
   LAUNCH_CHECK_();
 }
 
@@ -483,6 +527,118 @@ __global__ __launch_bounds__(256) void k_fb_c(MvDesc X, int j, const IcgsState *
   block_reduce_store<1>(v, 1, partial);
 }
 
+// Two passes per column instead of three.  The first projection of column j+1 onto the
+// basis is accumulated in the same pass that finishes column j (k_fb_ca), against column j
+// before its normalisation: <x2_j, X_{j+1}> is scaled by 1/diag_j afterwards (k_fb_scalar
+// stage 6), and column j is normalised on the fly by the next pass (k_fb_b2), which also
+// writes it back -- the same x2_j * (1/diag_j) the reference stores.
+//
+// (a01) partials [oldDot_0, oldDot_1, <X_0, X_1>] with X_0 not yet normalised.
+__global__ __launch_bounds__(256) void k_fb_a01(MvDesc X, int nrows, double *__restrict__ partial) {
+  double v[3] = {0.0, 0.0, 0.0};
+  const double *x0 = colp_(X, 0), *x1 = colp_(X, 1);
+  for (long long r = 2LL * ((long long)blockIdx.x * 256 + threadIdx.x); r < nrows;
+       r += 2LL * gridDim.x * 256) {
+    const d2 a = *(const d2 *)(x0 + r);
+    const d2 b = *(const d2 *)(x1 + r);
+    v[0] += a.x * a.x + a.y * a.y;
+    v[1] += b.x * b.x + b.y * b.y;
+    v[2] += a.x * b.x + a.y * b.y;
+  }
+  block_reduce_store<3>(v, 3, partial);
+}
+
+// (b2) normalise column j-1 in place (x * inv[j-1]); x1 = X_j - sum_i X_i P_i -> S;
+// partials <X_i, x1> (i < j), X_{j-1} taken normalised.
+__global__ __launch_bounds__(256) void k_fb_b2(MvDesc X, int j, const IcgsState *__restrict__ st,
+                                               double *__restrict__ S, int nrows, double *__restrict__ partial) {
+  double v[16];
+  double P[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    v[i] = 0.0;
+    P[i] = i < j ? st->P[i] : 0.0;
+  }
+  const double invp = st->inv[j - 1];
+  const double *xj = colp_(X, j);
+  double *xprev = colp_(X, j - 1);
+  for (long long r = 2LL * ((long long)blockIdx.x * 256 + threadIdx.x); r < nrows;
+       r += 2LL * gridDim.x * 256) {
+    d2 q[16];
+    double t0 = 0.0, t1 = 0.0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (i < j) {
+        q[i] = *(const d2 *)(colp_(X, i) + r);
+        if (i == j - 1) {
+          q[i].x = invp * q[i].x;
+          q[i].y = invp * q[i].y;
+        }
+        t0 += q[i].x * P[i];
+        t1 += q[i].y * P[i];
+      }
+    // write the normalised column back (the padding row of an odd tail is not written)
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (i == j - 1) {
+        xprev[r] = q[i].x;
+        if (r + 1 < nrows) xprev[r + 1] = q[i].y;
+      }
+    const d2 x = *(const d2 *)(xj + r);
+    const double a0 = x.x - t0, a1 = x.y - t1;
+    S[r] = a0;
+    if (r + 1 < nrows) S[r + 1] = a1;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (i < j) v[i] += q[i].x * a0 + q[i].y * a1;
+  }
+  block_reduce_store<16>(v, j, partial);
+}
+
+// (ca) x2 = S - sum_i X_i P2_i -> X_j (not normalised); partials
+// [newDot_j = <x2, X_j old>, and if j + 1 < k: oldDot_{j+1}, <X_i, X_{j+1}> (i < j), <x2, X_{j+1}>]
+__global__ __launch_bounds__(256) void k_fb_ca(MvDesc X, int j, int has_next, const IcgsState *__restrict__ st,
+                                               const double *__restrict__ S, int nrows,
+                                               double *__restrict__ partial) {
+  double v[17];
+#pragma unroll
+  for (int i = 0; i < 17; ++i) v[i] = 0.0;
+  double P[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) P[i] = i < j ? st->P2[i] : 0.0;
+  double *xj = colp_(X, j);
+  const double *xn = colp_(X, has_next ? j + 1 : j);
+  for (long long r = 2LL * ((long long)blockIdx.x * 256 + threadIdx.x); r < nrows;
+       r += 2LL * gridDim.x * 256) {
+    d2 q[16];
+    double t0 = 0.0, t1 = 0.0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (i < j) {
+        q[i] = *(const d2 *)(colp_(X, i) + r);
+        t0 += q[i].x * P[i];
+        t1 += q[i].y * P[i];
+      }
+    const d2 sv = *(const d2 *)(S + r);
+    const d2 old = *(const d2 *)(xj + r);
+    const double a0 = sv.x - t0, a1 = sv.y - t1;
+    v[0] += a0 * old.x + a1 * old.y;
+    xj[r] = a0;
+    if (r + 1 < nrows) xj[r + 1] = a1;
+    if (has_next) {
+      const d2 nx = *(const d2 *)(xn + r);
+      v[1] += nx.x * nx.x + nx.y * nx.y;
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        if (i < j) v[2 + i] += q[i].x * nx.x + q[i].y * nx.y;
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        if (i == j) v[2 + i] += a0 * nx.x + a1 * nx.y;
+    }
+  }
+  block_reduce_store<17>(v, has_next ? j + 3 : 1, partial);
+}
+
 __global__ __launch_bounds__(256) void k_scale_col(MvDesc X, int j, const IcgsState *__restrict__ st, int nrows) {
   const long long r = (long long)blockIdx.x * 256 + threadIdx.x;
   if (r < nrows) {
@@ -535,6 +691,41 @@ __global__ void k_fb_scalar(IcgsState *st, const double *__restrict__ red, int s
     // red = newDot (k values); oldDot from the Gram block recorded earlier
     for (int c = 0; c < k; ++c)
       if (fabs(red[c]) < fabs(st->blk_old[c] * st->blk_tol)) st->dep = 1.0;
+  } else if (stage == 5) {
+    // after k_fb_a01: column 0 (no projection) and the first projection of column 1
+    st->oldDot[0] = red[0];
+    st->oldDot[1] = red[1];
+    if (red[0] < 0.0 || red[1] < 0.0) st->neg = 1.0;
+    const double nd = red[0];
+    st->newDot[0] = nd;
+    const double tol = complete ? st->sing_tol : st->blk_tol;
+    const bool dep = complete ? fabs(nd) < fabs(tol * nd) : fabs(nd) < fabs(nd * tol);
+    if (dep && st->failed < 0) st->failed = 0;
+    const double diag = sqrt(fabs(nd));
+    st->diag[0] = diag;
+    st->inv[0] = 1.0 / diag;
+    st->B[0] = diag;
+    st->P[0] = red[2] * st->inv[0];
+    st->prod[0] = st->P[0];
+  } else if (stage == 6) {
+    // after k_fb_ca: finish column j as stage 2, then column j+1's first projection
+    const double nd = red[0];
+    st->newDot[j] = nd;
+    const double tol = complete ? st->sing_tol : st->blk_tol;
+    const bool dep = complete ? fabs(nd) < fabs(tol * st->oldDot[j]) : fabs(nd) < fabs(st->oldDot[j] * tol);
+    if (dep && st->failed < 0) st->failed = j;
+    const double diag = sqrt(fabs(nd));
+    st->diag[j] = diag;
+    st->inv[j] = 1.0 / diag;
+    st->B[j + 16 * j] = diag;
+    for (int i = 0; i < j; ++i) st->B[i + 16 * j] = st->prod[i];
+    if (j + 1 < k) {
+      st->oldDot[j + 1] = red[1];
+      if (red[1] < 0.0) st->neg = 1.0;
+      for (int i = 0; i < j; ++i) st->P[i] = red[2 + i];
+      st->P[j] = red[2 + j] * st->inv[j];
+      for (int i = 0; i <= j; ++i) st->prod[i] = st->P[i];
+    }
   } else if (stage == 4) {
     const double d = red[0];
     const double b = sqrt(fabs(d));
@@ -581,6 +772,19 @@ void launch_fb_b(hipStream_t s, MvDesc X, int j, const IcgsState *st, double *S,
 void launch_fb_c(hipStream_t s, MvDesc X, int j, const IcgsState *st, const double *S, int nrows, double *partial,
                  int nb) {
   k_fb_c<<<nb, 256, 0, s>>>(X, j, st, S, nrows, partial);
+  LAUNCH_CHECK_();
+}
+void launch_fb_a01(hipStream_t s, MvDesc X, int nrows, double *partial, int nb) {
+  k_fb_a01<<<nb, 256, 0, s>>>(X, nrows, partial);
+  LAUNCH_CHECK_();
+}
+void launch_fb_b2(hipStream_t s, MvDesc X, int j, const IcgsState *st, double *S, int nrows, double *partial, int nb) {
+  k_fb_b2<<<nb, 256, 0, s>>>(X, j, st, S, nrows, partial);
+  LAUNCH_CHECK_();
+}
+void launch_fb_ca(hipStream_t s, MvDesc X, int j, int has_next, const IcgsState *st, const double *S, int nrows,
+                  double *partial, int nb) {
+  k_fb_ca<<<nb, 256, 0, s>>>(X, j, has_next, st, S, nrows, partial);
   LAUNCH_CHECK_();
 }
 void launch_scale_col(hipStream_t s, MvDesc X, int j, const IcgsState *st, int nrows) {

@@ -262,7 +262,11 @@ migmres_mv *mv_create(migmres_ctx *ctx, long long n_global, int n_local, int nco
   m->n_global = n_global;
   m->n_local = n_local;
   m->ncols = ncols;
-  m->ld = round_up(n_local > 0 ? n_local : 1, 64);
+  // rows padded to a multiple of 64 (whole 64-row chunks, kept zero) plus 64 more rows so
+  // that columns are not a power-of-two distance apart: with ld = 2^24 every column's row r
+  // fell on the same HBM channel, and k_gemm_tn ran at 5.4 instead of 5.8-7.5 TB/s
+  // (tools/mb_lib.cpp, 256^3).
+  m->ld = round_up(n_local > 0 ? n_local : 1, 64) + 64;
   m->owner = true;
   const size_t bytes = (size_t)m->ld * (size_t)(ncols > 0 ? ncols : 1) * sizeof(double) + 256;
   try {

@@ -255,20 +255,22 @@ struct FastIcgs {
   long long n_global = 0;
   int nblk_tn = 1, nblk_ic = 1;
   double *partial = nullptr, *R1 = nullptr, *R2 = nullptr, *Cout = nullptr, *red = nullptr, *S = nullptr;
+  double *sink = nullptr;  // absorbs the padding-lane stores of the fused update kernel
   IcgsState *st = nullptr;
   double *h = nullptr;  // pinned: state + C
   MvPtr tmpX;
   long long calls = 0, fallbacks = 0;
   bool use_fused = true;  // MIGMRES_NO_FUSED_NN_TN=1 selects the two-kernel form (A/B timing)
-  int nt_cache[257] = {};
+  int nt_cache[257][4] = {};
 
   ~FastIcgs() { release(); }
   void release() {
     if (ctx) hipStreamSynchronize(ctx->stream);
-    for (void *p : {(void *)partial, (void *)R1, (void *)R2, (void *)Cout, (void *)red, (void *)S, (void *)st})
+    for (void *p : {(void *)partial, (void *)R1, (void *)R2, (void *)Cout, (void *)red, (void *)S, (void *)st,
+                    (void *)sink})
       if (p) hipFree(p);
     if (h) hipHostFree(h);
-    partial = R1 = R2 = Cout = red = S = nullptr;
+    partial = R1 = R2 = Cout = red = S = sink = nullptr;
     st = nullptr;
     h = nullptr;
     tmpX.reset();
@@ -286,16 +288,18 @@ struct FastIcgs {
     Lmax = lmax;
     nblk_tn = gemm_tn_blocks(nl);
     nblk_ic = icgs_blocks(nl);
-    for (int &v : nt_cache) v = 0;
+    for (auto &row : nt_cache)
+      for (int &v : row) v = 0;
     const char *nf = std::getenv("MIGMRES_NO_FUSED_NN_TN");
     use_fused = !(nf && nf[0] == '1');
     const size_t np = std::max({(size_t)nblk_tn * 512 * 16, (size_t)nblk_ic * 17,
-                                (size_t)nn_tn_blocks(nl, 16) * 256 * 16});
+                                (size_t)nn_tn_blocks(nl, 16, 1) * 256 * 16});
     MIG_HIP(hipMalloc(&partial, sizeof(double) * np));
     MIG_HIP(hipMalloc(&R1, sizeof(double) * (size_t)(lmax + k) * k));
     MIG_HIP(hipMalloc(&R2, sizeof(double) * (size_t)(lmax + k) * k));
     MIG_HIP(hipMalloc(&Cout, sizeof(double) * (size_t)(lmax + k) * k));
     MIG_HIP(hipMalloc(&red, sizeof(double) * 64));
+    MIG_HIP(hipMalloc(&sink, sizeof(double) * 256 * (size_t)nn_tn_blocks(nl, 16, 1)));
     const size_t sbytes = sizeof(double) * ((size_t)(nl > 0 ? nl : 1) + 64);
     MIG_HIP(hipMalloc(&S, sbytes));
     MIG_HIP(hipMemset(S, 0, sbytes));  // zero padding row read by the row-pair kernels
@@ -348,14 +352,14 @@ struct FastIcgs {
   // X = X - Q C1 (C1 leading dim ldc1) then out = Q^T X, summed over ranks: one fused pass
   // over Q when the shape allows it, else MvTimesMatAddMv followed by MvTransMv.
   void nn_then_tn(const MvDesc &Q, int L, const double *C1, int ldc1, const MvDesc &X, int k, double *out) {
-    // Measured at 256^3, k = 8 (tools/mb_lib.cpp): the fused kernel is fp64-MFMA bound and
-    // wins over the two streaming kernels only for 32 <= L <= 64 and L >= 160.
-    const bool fused_wins = (L >= 32 && L <= 64) || L >= 160;
+    // Measured at 256^3, k = 8 (tools/mb_lib.cpp): the fused kernel beats the two streaming
+    // kernels from L = 16 on (1.3 vs 1.4 ms at L = 16, 9.0 vs 10.5 ms at L = 200).
+    const bool fused_wins = L >= 16;
     if (use_fused && fused_wins && !Q.cols && nn_tn_supported(L, k)) {
-      const int nb = nt_blocks(L);
+      const int nb = nt_blocks(L, k);
       {
         ProfScope ps(ctx, K_NN_TN, 8.0 * n_local * (L + 2.0 * k) + 8.0 * nb * L * k);
-        launch_nn_tn(ctx->stream, Q, L, C1, ldc1, X, n_local, partial, nb);
+        launch_nn_tn(ctx->stream, Q, L, C1, ldc1, X, n_local, partial, nb, sink);
       }
       {
         ProfScope ps(ctx, K_REDUCE, 8.0 * nb * L * k);
@@ -368,33 +372,43 @@ struct FastIcgs {
     tn(Q, L, X, k, out, L);
   }
 
-  int nt_blocks(int L) {
-    if (nt_cache[L] == 0) nt_cache[L] = nn_tn_blocks(n_local, L);
-    return nt_cache[L];
+  int nt_blocks(int L, int k) {
+    int &v = nt_cache[L][(k + 3) / 4 - 1];
+    if (v == 0) v = nn_tn_blocks(n_local, L, k);
+    return v;
   }
 
   void find_basis(const MvDesc &X, int k, int complete) {
     const double n = (double)n_local;
-    for (int j = 0; j < k; ++j) {
+    if (k == 1) {
       {
-        ProfScope ps(ctx, K_FB, 8.0 * n * (j + 1) + (j > 0 ? 8.0 * n : 0.0));
-        launch_fb_a(ctx->stream, X, j, st, n_local, partial, nblk_ic);
-      }
-      reduce_small(j + 1);
-      launch_fb_scalar(ctx->stream, st, red, 0, j, k, complete);
-      if (j == 0) continue;
-      {
-        ProfScope ps(ctx, K_FB, 8.0 * n * (j + 2));
-        launch_fb_b(ctx->stream, X, j, st, S, n_local, partial, nblk_ic);
-      }
-      reduce_small(j);
-      launch_fb_scalar(ctx->stream, st, red, 1, j, k, complete);
-      {
-        ProfScope ps(ctx, K_FB, 8.0 * n * (j + 3));
-        launch_fb_c(ctx->stream, X, j, st, S, n_local, partial, nblk_ic);
+        ProfScope ps(ctx, K_FB, 8.0 * n);
+        launch_fb_a(ctx->stream, X, 0, st, n_local, partial, nblk_ic);
       }
       reduce_small(1);
-      launch_fb_scalar(ctx->stream, st, red, 2, j, k, complete);
+      launch_fb_scalar(ctx->stream, st, red, 0, 0, k, complete);
+    } else {
+      {
+        ProfScope ps(ctx, K_FB, 16.0 * n);
+        launch_fb_a01(ctx->stream, X, n_local, partial, nblk_ic);
+      }
+      reduce_small(3);
+      launch_fb_scalar(ctx->stream, st, red, 5, 0, k, complete);
+      for (int j = 1; j < k; ++j) {
+        {
+          ProfScope ps(ctx, K_FB, 8.0 * n * (j + 3));
+          launch_fb_b2(ctx->stream, X, j, st, S, n_local, partial, nblk_ic);
+        }
+        reduce_small(j);
+        launch_fb_scalar(ctx->stream, st, red, 1, j, k, complete);
+        const int has_next = j + 1 < k;
+        {
+          ProfScope ps(ctx, K_FB, 8.0 * n * (j + 3 + has_next));
+          launch_fb_ca(ctx->stream, X, j, has_next, st, S, n_local, partial, nblk_ic);
+        }
+        reduce_small(has_next ? j + 3 : 1);
+        launch_fb_scalar(ctx->stream, st, red, 6, j, k, complete);
+      }
     }
     ProfScope ps(ctx, K_SCALE, 16.0 * n);
     launch_scale_col(ctx->stream, X, k - 1, st, n_local);
