@@ -201,8 +201,8 @@ void launch_gemm_nn_dot(hipStream_t s, MvDesc A, int L, const double *M, int ldm
 // LDS: Qs[Lp][17] (odd stride: both phases' reads are conflict-free), Xs[16][16], red[4][4][64].
 // -------------------------------------------------------------------------------------
 constexpr int NT_ROWS = 16, NT_MAXL = 256, NT_LDQ = 17;
-#ifndef NT_DIAG_MASK  // bit 0 phase 1, bit 1 phase 2, bit 2 LDS staging (tools/mb_nntn.hip)
-#define NT_DIAG_MASK 7
+#ifndef NT_DIAG_MASK  // bit 0 phase 1, bit 1 phase 2, bit 2 LDS staging, bit 3 X1 traffic (tools/mb_nntn.hip)
+#define NT_DIAG_MASK 15
 #endif
 
 static size_t nt_lds_bytes(int L) {
@@ -324,9 +324,9 @@ __global__ __launch_bounds__(256, 2) void k_nn_tn(MvDesc Q, int L, const double 
       const bool ok = xcol_ok && live && r0 + xrow < nrows;
       const double x1 = ok ? xv - d : 0.0;
       double *dst = ok ? xdst + r0 + xrow : sink + (blockIdx.x * 256 + t);
-      *dst = x1;
+      if (NT_DIAG_MASK & 8) *dst = x1;
       Xs[xrow * 16 + xc] = x1;
-      loadx(xv, chunk + 2 * G);
+      if (NT_DIAG_MASK & 8) loadx(xv, chunk + 2 * G);
     }
     lds_barrier();
     // phase 2: acc[tile][jg] += Q[:, tile]^T X1[:, 4 jg .. 4 jg + 3] over the 16 rows
@@ -375,6 +375,128 @@ __global__ __launch_bounds__(256, 2) void k_nn_tn(MvDesc Q, int L, const double 
   }
 }
 
+// Wide variant for k <= 8: one 1024-thread workgroup per CU stages 64-row chunks (512 B
+// per Q column per visit instead of 128 B: with 16-row chunks the Q stream alone, no
+// compute, fell from 6.4 TB/s at L = 64 to 3.7 TB/s at L = 200, tools/mb_nntn.hip).
+//   phase 1: wave w = (row block rb = w & 3, K quarter kq = w >> 2) forms a 16 x k partial
+//            of Qc C1; the 4 K quarters are summed in a fixed order by the X1 owners,
+//   X1:      wave w owns column w of the chunk's 64 rows (one 512-B load and store),
+//   phase 2: wave w accumulates Q tile w (16 columns) against X1 over the 64 rows.
+// LDS: Qs[Lp][65] | Xs[64][16] | red[16][NJ][64] | C1s[Lp][4 NJ]; 1-deep register prefetch.
+constexpr int NW_ROWS = 64, NW_LDQ = 65;
+
+static size_t nw_lds_bytes(int L, int NJ) {
+  const int Lp = (L + 15) & ~15;
+  return sizeof(double) * ((size_t)Lp * NW_LDQ + 64 * 16 + 16 * NJ * 64 + (size_t)Lp * 4 * NJ);
+}
+
+template <int NM, int NJ>
+__global__ __launch_bounds__(1024, 1) void k_nn_tn_w(MvDesc Q, int L, const double *__restrict__ C1, int ldc,
+                                                     MvDesc X, int k, int nrows, double *__restrict__ partial,
+                                                     double *__restrict__ sink) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const int Lp = (L + 15) & ~15;
+  double *Qs = sm;
+  double *Xs = sm + (size_t)Lp * NW_LDQ;
+  double *red = Xs + 64 * 16;
+  double *C1s = red + 16 * NJ * 64;  // [Lp][4 NJ], zero past L and k
+  const int t = threadIdx.x, w = t >> 6, l = t & 63, c = l & 15, g = l >> 4, n4 = l & 3;
+  const int rb = w & 3, kq = w >> 2;
+  for (int e = t; e < (Lp - L) * NW_LDQ; e += 1024) Qs[L * NW_LDQ + e] = 0.0;
+  for (int e = t; e < Lp * 4 * NJ; e += 1024) {
+    const int i = e / (4 * NJ), j = e % (4 * NJ);
+    C1s[e] = (i < L && j < k) ? C1[i + (long long)j * ldc] : 0.0;
+  }
+  double acc2[NJ];
+#pragma unroll
+  for (int jg = 0; jg < NJ; ++jg) acc2[jg] = 0.0;
+
+  // loader: column lcol + 32 m (clamped), rows 2 (t & 31) and + 1 of the 64-row chunk
+  const int lrow = 2 * (t & 31), lcol = t >> 5;
+  auto scol = [&](int m) { const int i = lcol + 32 * m; return i < L ? i : L - 1; };
+  const double *qb = Q.base + lrow;
+  const long long qld = Q.ld;
+  // X1 owner: row l of the chunk in column w (columns >= k store into the sink)
+  const bool xok_col = w < k;
+  const double *xsrc = colp_(X, xok_col ? w : k - 1);
+  double *xdst = colp_(X, xok_col ? w : k - 1);
+  const int xjg = (w >> 2) < NJ ? (w >> 2) : NJ - 1;
+  const int xo = 16 * (l & 3) + 4 * ((l >> 2) & 3) + (w & 3);  // D lane of (row l & 15, column w)
+  const int xrb = l >> 4;
+  const long long nchunks = (nrows + NW_ROWS - 1) / NW_ROWS;
+  const long long G = gridDim.x;
+  auto clampc = [&](long long chunk) { return chunk < nchunks ? chunk : nchunks - 1; };
+
+  d2 p[NM];
+  double xv;
+  {
+    const long long c0 = clampc(blockIdx.x);
+#pragma unroll
+    for (int m = 0; m < NM; ++m) p[m] = *(const d2 *)(qb + scol(m) * qld + c0 * NW_ROWS);
+    xv = xsrc[c0 * NW_ROWS + l];
+  }
+  for (long long ch = blockIdx.x; ch < nchunks; ch += G) {
+    const long long r0 = ch * NW_ROWS;
+#pragma unroll
+    for (int m = 0; m < NM; ++m) {
+      Qs[scol(m) * NW_LDQ + lrow] = p[m].x;
+      Qs[scol(m) * NW_LDQ + lrow + 1] = p[m].y;
+    }
+    const double xcur = xv;
+    lds_barrier();
+    {
+      const long long cn = clampc(ch + G);
+#pragma unroll
+      for (int m = 0; m < NM; ++m) p[m] = *(const d2 *)(qb + scol(m) * qld + cn * NW_ROWS);
+      xv = xsrc[cn * NW_ROWS + l];
+    }
+    // phase 1: rows 16 rb .. 16 rb + 15, K steps s = kq + 4 m
+    double a1[NJ];
+#pragma unroll
+    for (int jg = 0; jg < NJ; ++jg) a1[jg] = 0.0;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      const int s = kq + 4 * m;
+      if (4 * s < L) {
+        const double qa = Qs[(4 * s + g) * NW_LDQ + 16 * rb + c];
+#pragma unroll
+        for (int jg = 0; jg < NJ; ++jg) a1[jg] = mfma4(qa, C1s[(4 * s + g) * 4 * NJ + 4 * jg + n4], a1[jg]);
+      }
+    }
+#pragma unroll
+    for (int jg = 0; jg < NJ; ++jg) red[((kq * 4 + rb) * NJ + jg) * 64 + l] = a1[jg];
+    lds_barrier();
+    {
+      const double d = (red[((0 * 4 + xrb) * NJ + xjg) * 64 + xo] + red[((1 * 4 + xrb) * NJ + xjg) * 64 + xo]) +
+                       (red[((2 * 4 + xrb) * NJ + xjg) * 64 + xo] + red[((3 * 4 + xrb) * NJ + xjg) * 64 + xo]);
+      const bool ok = xok_col && ch < nchunks && r0 + l < nrows;
+      const double x1 = ok ? xcur - d : 0.0;
+      double *dst = ok ? xdst + r0 + l : sink + t;
+      *dst = x1;
+      Xs[l * 16 + w] = x1;
+    }
+    lds_barrier();
+    // phase 2: tile w (Q columns 16 w .. 16 w + 15) against the 64 rows of X1
+    if (16 * w < L) {
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const double qa = Qs[(16 * w + c) * NW_LDQ + 4 * s + g];
+#pragma unroll
+        for (int jg = 0; jg < NJ; ++jg) acc2[jg] = mfma4(qa, Xs[(4 * s + g) * 16 + 4 * jg + n4], acc2[jg]);
+      }
+    }
+    lds_barrier();
+  }
+  // partial (L x k) of this workgroup: tile w rows 16 w + 4 b + m
+  double *out = partial + (long long)blockIdx.x * L * k;
+  const int i = 16 * w + 4 * ((l >> 2) & 3) + (l >> 4);
+#pragma unroll
+  for (int jg = 0; jg < NJ; ++jg) {
+    const int j = 4 * jg + n4;
+    if (16 * w < L && i < L && j < k) out[i + (long long)j * L] = acc2[jg];
+  }
+}
+
 typedef void (*nt_kernel_t)(MvDesc, int, const double *, int, MvDesc, int, int, double *, double *);
 
 template <int NJ>
@@ -400,17 +522,47 @@ static nt_kernel_t nt_pick(int L, int k) {
   }
 }
 
-int nn_tn_blocks(int nrows, int L, int k) {
-  int per_cu = 0, dev = 0, cus = 0;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nt_pick(L, k), 256, nt_lds_bytes(L)) != hipSuccess ||
-      per_cu < 1 || cus < 1) {
-    per_cu = 2;
-    cus = 256;
+template <int NJ>
+static nt_kernel_t nw_pick_nm(int L) {
+  switch ((L + 31) >> 5) {
+    case 1: return k_nn_tn_w<1, NJ>;
+    case 2: return k_nn_tn_w<2, NJ>;
+    case 3: return k_nn_tn_w<3, NJ>;
+    case 4: return k_nn_tn_w<4, NJ>;
+    case 5: return k_nn_tn_w<5, NJ>;
+    case 6: return k_nn_tn_w<6, NJ>;
+    case 7: return k_nn_tn_w<7, NJ>;
+    default: return k_nn_tn_w<8, NJ>;
   }
+}
+
+// The wide variant wins from L = 64 on (4.6 vs 3.4 TB/s at L = 64 and 200, 256^3 k = 8);
+// below that one workgroup per CU cannot hide the per-chunk latency.
+static bool nw_ok(int L, int k) { return L >= 64 && k <= 8 && nw_lds_bytes(L, (k + 3) >> 2) <= 160 * 1024; }
+
+static int cu_count() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+      cus = 256;
+  }
+  return cus;
+}
+
+int nn_tn_blocks(int nrows, int L, int k) {
+  if (nw_ok(L, k)) {
+    const long long nchunks = (nrows + NW_ROWS - 1) / NW_ROWS;
+    const long long b = cu_count() < nchunks ? cu_count() : nchunks;
+    return b < 1 ? 1 : (int)b;
+  }
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nt_pick(L, k), 256, nt_lds_bytes(L)) != hipSuccess ||
+      per_cu < 1)
+    per_cu = 2;
   const long long nchunks = (nrows + NT_ROWS - 1) / NT_ROWS;
-  long long b = (long long)per_cu * cus;
+  long long b = (long long)per_cu * cu_count();
   if (b > nchunks) b = nchunks;
   return b < 1 ? 1 : (int)b;
 }
@@ -422,8 +574,22 @@ void launch_nn_tn(hipStream_t s, MvDesc Q, int L, const double *C1, int ldc, MvD
   const int k = X.ncols;
   if (!nn_tn_supported(L, k)) throw Error(MIGMRES_EINVAL, "nn_tn: 1 <= L <= 256 and 1 <= k <= 16");
   if (Q.cols) throw Error(MIGMRES_EINVAL, "nn_tn: Q must be a contiguous column range");
-  hipLaunchKernelGGL(nt_pick(L, k), dim3(nblocks), dim3(256), nt_lds_bytes(L), s, Q, L, C1, ldc, X, k, nrows,
-                     partial, sink);
+  if (nw_ok(L, k)) {
+    const int NJ = (k + 3) >> 2;
+    nt_kernel_t f = NJ == 1 ? nw_pick_nm<1>(L) : nw_pick_nm<2>(L);
+    const size_t lds = nw_lds_bytes(L, NJ);
+    static bool attr_set[2][9] = {};
+    const int nm = (L + 31) >> 5;
+    if (!attr_set[NJ - 1][nm]) {
+      if (hipFuncSetAttribute((const void *)f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+        throw Error(MIGMRES_EHIP, "nn_tn: cannot raise the dynamic LDS limit");
+      attr_set[NJ - 1][nm] = true;
+    }
+    hipLaunchKernelGGL(f, dim3(nblocks), dim3(1024), lds, s, Q, L, C1, ldc, X, k, nrows, partial, sink);
+  } else {
+    hipLaunchKernelGGL(nt_pick(L, k), dim3(nblocks), dim3(256), nt_lds_bytes(L), s, Q, L, C1, ldc, X, k, nrows,
+                       partial, sink);
+  }
   LAUNCH_CHECK_();
 }
 
