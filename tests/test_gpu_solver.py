@@ -175,3 +175,46 @@ def test_reference_pinned_runs(comm, name):
     np.testing.assert_allclose(rel, gold["true_rel"], rtol=1e-3)
     if name.startswith("laplace3d_64"):
         assert meta["iterations"] == 201 and meta["n_apply"] + 1 == 268 and meta["n_explicit"] == 61
+
+
+def test_dependent_blocks_blkorthosing(comm):
+    """One right-hand side is an eigenvector of a diagonal operator, so blocks keep
+    carrying a dependent direction: ICGS takes blkOrthoSing (random vectors from the
+    MvRandom stream) five times -- on the device path that is the fallback that regenerates
+    the block by repeating the SpMM (no input copy).  (A problem whose Krylov space is
+    exhausted outright is not a parity case: after exhaustion the dependency decisions are
+    made on rounding noise, so they differ between any two summation orders.)"""
+    import trilinos_amd as ta
+    from oracle import belos as ob, epetra as oe
+    n, k = 400, 4
+    vals = 1.0 + np.arange(n) * 0.05
+
+    def gen(f, m):
+        return np.arange(m + 1), np.arange(f, f + m), vals[f:f + m].copy()
+
+    Aor = oe.DistCrs(gen, n, 1)
+    Xe, _ = oe.epetra_random_mv(3, n, k)
+    Xe[:, 0] = 0.0
+    Xe[5, 0] = 1.0
+    Bh = Aor.apply(Xe)
+    params = {"Num Blocks": 20, "Block Size": k, "Maximum Iterations": 200, "Maximum Restarts": 5,
+              "Convergence Tolerance": 1e-8, "Orthogonalization": "ICGS"}
+    ref = ob.solve(Aor.apply, Bh, params)
+    assert ref["blk_ortho_sing"] == 5
+    rp, gc, vv = gen(0, n)
+    A = ta.CrsMatrix(comm, n, rp, gc, vv)
+    B = ta.MultiVector(comm, n, k)
+    B.upload(Bh)
+    X = ta.MultiVector(comm, n, k)
+    X.put_scalar(0.0)
+    lp = ta.LinearProblem(A, X, B)
+    assert lp.setProblem()
+    sm = ta.BlockGmresSolMgr(lp, params)
+    ret = sm.solve()
+    c = sm.counters()
+    assert (ret == ta.Converged) == ref["converged"]
+    assert sm.getNumIters() == ref["iterations"]
+    assert c["restarts"] == ref["restarts"] and c["applies"] == ref["n_apply"]
+    assert c["explicit_checks"] == ref["n_explicit"]
+    assert c["blk_ortho_sing"] == ref["blk_ortho_sing"]
+    _hist_close(sm.residualHistory(), ref["history"], ref["restarts"])

@@ -38,6 +38,9 @@ void launch_fb_b2(hipStream_t s, MvDesc X, int j, const IcgsState *st, double *S
 void launch_fb_ca(hipStream_t s, MvDesc X, int j, int has_next, const IcgsState *st, const double *S, int nrows,
                   double *partial, int nb);
 void launch_scale_col(hipStream_t s, MvDesc X, int j, const IcgsState *st, int nrows);
+// reduce_small followed by fb_scalar in one single-workgroup launch (single rank only)
+void launch_reduce_scalar(hipStream_t s, const double *partial, int nblocks, int nv, double *red, IcgsState *st,
+                          int stage, int j, int k, int complete);
 void launch_fb_scalar(hipStream_t s, IcgsState *st, const double *red, int stage, int j, int k, int complete);
 void launch_blk_old(hipStream_t s, IcgsState *st, const double *G, int ldg, int L, int k);
 void launch_state_reset(hipStream_t s, IcgsState *st, double blk_tol, double sing_tol);

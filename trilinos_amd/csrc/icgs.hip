@@ -109,34 +109,43 @@ __global__ __launch_bounds__(256) void k_gemm_nn_dot(MvDesc A, int L, const doub
     Ms[e] = c < kx ? M[j + (long long)c * ldm] : 0.0;
   }
   __syncthreads();
-  double dacc[KX];
+  double dacc[KX + 1];  // dmode 3: [KX] = <Xnew_0, Xnew_1> (findBasis head, see k_fb_scalar stage 7)
 #pragma unroll
-  for (int c = 0; c < KX; ++c) dacc[c] = 0.0;
+  for (int c = 0; c <= KX; ++c) dacc[c] = 0.0;
   for (long long r = 2LL * ((long long)blockIdx.x * 256 + threadIdx.x); r < nrows;
        r += 2LL * gridDim.x * 256) {
     const bool two = r + 1 < nrows;
     double acc0[KX], acc1[KX];
 #pragma unroll
     for (int c = 0; c < KX; ++c) acc0[c] = acc1[c] = 0.0;
-#pragma unroll 4
-    for (int j = 0; j < L; ++j) {
-      const double *ap = colp_(A, j) + r;
-      double a0, a1;
-      if (two) {
-        const d2 v = *(const d2 *)ap;
-        a0 = v.x;
-        a1 = v.y;
-      } else {
-        a0 = ap[0];
-        a1 = 0.0;
+    // NB columns per step, all loads issued before the FMAs (more bytes in flight per wave);
+    // rows past nrows are the zero padding of the multivector (ld > nrows), read unguarded.
+    constexpr int NB = 8;
+    int j = 0;
+    for (; j + NB <= L; j += NB) {
+      d2 v[NB];
+#pragma unroll
+      for (int u = 0; u < NB; ++u) v[u] = *(const d2 *)(colp_(A, j + u) + r);
+#pragma unroll
+      for (int u = 0; u < NB; ++u) {
+        const double *mrow = &Ms[(j + u) * KX];
+#pragma unroll
+        for (int c = 0; c < KX; ++c) {
+          acc0[c] += v[u].x * mrow[c];
+          acc1[c] += v[u].y * mrow[c];
+        }
       }
+    }
+    for (; j < L; ++j) {
+      const d2 v = *(const d2 *)(colp_(A, j) + r);
       const double *mrow = &Ms[j * KX];
 #pragma unroll
       for (int c = 0; c < KX; ++c) {
-        acc0[c] += a0 * mrow[c];
-        acc1[c] += a1 * mrow[c];
+        acc0[c] += v.x * mrow[c];
+        acc1[c] += v.y * mrow[c];
       }
     }
+    double f0 = 0.0, f1 = 0.0;  // new column 0 (dmode 3)
 #pragma unroll
     for (int c = 0; c < KX; ++c) {
       if (c < kx) {
@@ -151,8 +160,16 @@ __global__ __launch_bounds__(256) void k_gemm_nn_dot(MvDesc A, int L, const doub
         }
         xp[0] = n0;
         if (two) xp[1] = n1;
-        if (dmode == 1) {
+        if (dmode == 1 || dmode == 3) {
           dacc[c] += n0 * n0 + n1 * n1;
+          if (dmode == 3) {
+            if (c == 0) {
+              f0 = n0;
+              f1 = n1;
+            } else if (c == 1) {
+              dacc[KX] += f0 * n0 + f1 * n1;
+            }
+          }
         } else if (dmode == 2) {
           const double *dp = colp_(D, c) + r;
           dacc[c] += n0 * dp[0] + (two ? n1 * dp[1] : 0.0);
@@ -160,7 +177,15 @@ __global__ __launch_bounds__(256) void k_gemm_nn_dot(MvDesc A, int L, const doub
       }
     }
   }
-  if (dmode) block_reduce_store<KX>(dacc, kx, partial);
+  if (dmode == 3) {
+    // compact [self dots (kx), cross] for the partial layout
+#pragma unroll
+    for (int c = 0; c < KX; ++c)
+      if (c == kx) dacc[c] = dacc[KX];
+    block_reduce_store<KX + 1>(dacc, kx + 1, partial);
+  } else if (dmode) {
+    block_reduce_store<KX + 1>(dacc, kx, partial);
+  }
 }
 
 void launch_gemm_nn_dot(hipStream_t s, MvDesc A, int L, const double *M, int ldm, MvDesc X,
@@ -816,9 +841,50 @@ __global__ __launch_bounds__(256) void k_scale_col(MvDesc X, int j, const IcgsSt
 // Scalar step after a reduction (red = reduced vector).  stage: 0 after (a), 1 after (b),
 // 2 after (c), 3 after blkOrtho's projections (C = C1 + C2, dependency test), 4 for the
 // k == 1 normalisation.
+__device__ void fb_scalar_body(IcgsState *st, const double *red, int stage, int j, int k, int complete);
+
 __global__ void k_fb_scalar(IcgsState *st, const double *__restrict__ red, int stage, int j, int k,
                             int complete) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  fb_scalar_body(st, red, stage, j, k, complete);
+}
+
+// Single-rank form of reduce_small + fb_scalar: one workgroup reduces the partials, then
+// its thread 0 takes the scalar step (saves a launch per findBasis step).
+__global__ __launch_bounds__(256) void k_reduce_scalar(const double *__restrict__ partial, int nblocks, int nv,
+                                                       double *__restrict__ out, IcgsState *st, int stage, int j,
+                                                       int k, int complete) {
+  double v[17];
+#pragma unroll
+  for (int i = 0; i < 17; ++i) v[i] = 0.0;
+  for (int b = threadIdx.x; b < nblocks; b += 256) {
+#pragma unroll
+    for (int i = 0; i < 17; ++i)
+      if (i < nv) v[i] += partial[(long long)b * nv + i];
+  }
+  __shared__ double red[4][17];
+  __shared__ double sum[17];
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < 17; ++i) {
+    if (i < nv) {
+      double x = v[i];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off, 64);
+      if (l == 0) red[w][i] = x;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < nv) {
+    const int i = threadIdx.x;
+    sum[i] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
+    out[i] = sum[i];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) fb_scalar_body(st, sum, stage, j, k, complete);
+}
+
+__device__ void fb_scalar_body(IcgsState *st, const double *red, int stage, int j, int k, int complete) {
   if (stage == 0) {
     st->oldDot[j] = red[0];
     if (st->oldDot[j] < 0.0) st->neg = 1.0;
@@ -872,6 +938,23 @@ __global__ void k_fb_scalar(IcgsState *st, const double *__restrict__ red, int s
     st->inv[0] = 1.0 / diag;
     st->B[0] = diag;
     st->P[0] = red[2] * st->inv[0];
+    st->prod[0] = st->P[0];
+  } else if (stage == 7) {
+    // findBasis head from blkOrtho's closing dots (dmode 3 of k_gemm_nn_dot): red[0], red[1]
+    // = <X_0, X_0>, <X_1, X_1>, red[k] = <X_0, X_1>; then as stage 5
+    st->oldDot[0] = red[0];
+    st->oldDot[1] = red[1];
+    if (red[0] < 0.0 || red[1] < 0.0) st->neg = 1.0;
+    const double nd = red[0];
+    st->newDot[0] = nd;
+    const double tol = complete ? st->sing_tol : st->blk_tol;
+    const bool dep = complete ? fabs(nd) < fabs(tol * nd) : fabs(nd) < fabs(nd * tol);
+    if (dep && st->failed < 0) st->failed = 0;
+    const double diag = sqrt(fabs(nd));
+    st->diag[0] = diag;
+    st->inv[0] = 1.0 / diag;
+    st->B[0] = diag;
+    st->P[0] = red[k] * st->inv[0];
     st->prod[0] = st->P[0];
   } else if (stage == 6) {
     // after k_fb_ca: finish column j as stage 2, then column j+1's first projection
@@ -956,6 +1039,11 @@ void launch_fb_ca(hipStream_t s, MvDesc X, int j, int has_next, const IcgsState 
 void launch_scale_col(hipStream_t s, MvDesc X, int j, const IcgsState *st, int nrows) {
   if (nrows <= 0) return;
   k_scale_col<<<cdiv_(nrows, 256), 256, 0, s>>>(X, j, st, nrows);
+  LAUNCH_CHECK_();
+}
+void launch_reduce_scalar(hipStream_t s, const double *partial, int nblocks, int nv, double *red, IcgsState *st,
+                          int stage, int j, int k, int complete) {
+  k_reduce_scalar<<<1, 256, 0, s>>>(partial, nblocks, nv, red, st, stage, j, k, complete);
   LAUNCH_CHECK_();
 }
 void launch_fb_scalar(hipStream_t s, IcgsState *st, const double *red, int stage, int j, int k, int complete) {

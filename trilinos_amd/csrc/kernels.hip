@@ -482,18 +482,27 @@ __global__ __launch_bounds__(256) void k_gemm_nn(MvDesc A, int L, const double *
     }
     __syncthreads();
     if (r < nrows) {
-#pragma unroll 4
-      for (int jj = 0; jj < jn; ++jj) {
-        const double *ap = colp(A, j0 + jj) + r;
-        double a0, a1;
-        if (two) {
-          const d2 v = *(const d2 *)ap;
-          a0 = v.x;
-          a1 = v.y;
-        } else {
-          a0 = ap[0];
-          a1 = 0.0;
+      // 8 columns' loads in flight before their FMAs; an odd tail row pairs with the zero
+      // padding row (every multivector has ld > n_local), read unguarded
+      int jj = 0;
+      for (; jj + 8 <= jn; jj += 8) {
+        d2 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = *(const d2 *)(colp(A, j0 + jj + u) + r);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const double *mrow = &Ms[(jj + u) * KX];
+#pragma unroll
+          for (int c = 0; c < KX; ++c) {
+            acc0[c] += v[u].x * mrow[c];
+            acc1[c] += v[u].y * mrow[c];
+          }
         }
+      }
+      for (; jj < jn; ++jj) {
+        const double *ap = colp(A, j0 + jj) + r;
+        const d2 v = *(const d2 *)ap;
+        const double a0 = v.x, a1 = v.y;
         const double *mrow = &Ms[jj * KX];
 #pragma unroll
         for (int c = 0; c < KX; ++c) {

@@ -13,6 +13,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <limits>
 #include <map>
 #include <memory>
@@ -338,15 +339,26 @@ struct FastIcgs {
     launch_reduce_small(ctx->stream, partial, nblk_ic, nvals, red);
     allreduce(red, (size_t)nvals);
   }
+  // reduce_small + the scalar step (one launch when there is no all-reduce in between)
+  void reduce_scalar(int nvals, int stage, int j, int k, int complete) {
+    if (ctx->nranks > 1) {
+      reduce_small(nvals);
+      launch_fb_scalar(ctx->stream, st, red, stage, j, k, complete);
+      return;
+    }
+    ProfScope ps(ctx, K_REDUCE, 8.0 * nblk_ic * nvals);
+    launch_reduce_scalar(ctx->stream, partial, nblk_ic, nvals, red, st, stage, j, k, complete);
+  }
 
-  void nn(const MvDesc &Q, int L, const double *M, int ldm, const MvDesc &X, int k, bool dot) {
+  // dot: 0 none, 1 column self dots, 3 self dots + <X_0, X_1>
+  void nn(const MvDesc &Q, int L, const double *M, int ldm, const MvDesc &X, int k, int dot) {
     if (!dot) {
       ProfScope ps(ctx, K_GEMM_NN, 8.0 * n_local * (L + 2.0 * k));
       launch_gemm_nn(ctx->stream, Q, L, M, ldm, X, n_local, -1.0, 1.0);
       return;
     }
     ProfScope ps(ctx, K_GEMM_NN_DOT, 8.0 * n_local * (L + 2.0 * k));
-    launch_gemm_nn_dot(ctx->stream, Q, L, M, ldm, X, n_local, -1.0, 1.0, 1, X, partial, nblk_ic);
+    launch_gemm_nn_dot(ctx->stream, Q, L, M, ldm, X, n_local, -1.0, 1.0, dot, X, partial, nblk_ic);
   }
 
   // X = X - Q C1 (C1 leading dim ldc1) then out = Q^T X, summed over ranks: one fused pass
@@ -368,7 +380,7 @@ struct FastIcgs {
       allreduce(out, (size_t)L * k);
       return;
     }
-    nn(Q, L, C1, ldc1, X, k, false);
+    nn(Q, L, C1, ldc1, X, k, 0);
     tn(Q, L, X, k, out, L);
   }
 
@@ -378,36 +390,38 @@ struct FastIcgs {
     return v;
   }
 
-  void find_basis(const MvDesc &X, int k, int complete) {
+  // head_ready: red already holds [<X_0,X_0>, <X_1,X_1>, ..., <X_0,X_1> at k] from the
+  // closing update of blkOrtho (k_gemm_nn_dot dmode 3), so the a01 pass is skipped.
+  void find_basis(const MvDesc &X, int k, int complete, bool head_ready = false) {
     const double n = (double)n_local;
     if (k == 1) {
       {
         ProfScope ps(ctx, K_FB, 8.0 * n);
         launch_fb_a(ctx->stream, X, 0, st, n_local, partial, nblk_ic);
       }
-      reduce_small(1);
-      launch_fb_scalar(ctx->stream, st, red, 0, 0, k, complete);
+      reduce_scalar(1, 0, 0, k, complete);
     } else {
-      {
-        ProfScope ps(ctx, K_FB, 16.0 * n);
-        launch_fb_a01(ctx->stream, X, n_local, partial, nblk_ic);
+      if (head_ready) {
+        launch_fb_scalar(ctx->stream, st, red, 7, 0, k, complete);
+      } else {
+        {
+          ProfScope ps(ctx, K_FB, 16.0 * n);
+          launch_fb_a01(ctx->stream, X, n_local, partial, nblk_ic);
+        }
+        reduce_scalar(3, 5, 0, k, complete);
       }
-      reduce_small(3);
-      launch_fb_scalar(ctx->stream, st, red, 5, 0, k, complete);
       for (int j = 1; j < k; ++j) {
         {
           ProfScope ps(ctx, K_FB, 8.0 * n * (j + 3));
           launch_fb_b2(ctx->stream, X, j, st, S, n_local, partial, nblk_ic);
         }
-        reduce_small(j);
-        launch_fb_scalar(ctx->stream, st, red, 1, j, k, complete);
+        reduce_scalar(j, 1, j, k, complete);
         const int has_next = j + 1 < k;
         {
           ProfScope ps(ctx, K_FB, 8.0 * n * (j + 3 + has_next));
           launch_fb_ca(ctx->stream, X, j, has_next, st, S, n_local, partial, nblk_ic);
         }
-        reduce_small(has_next ? j + 3 : 1);
-        launch_fb_scalar(ctx->stream, st, red, 6, j, k, complete);
+        reduce_scalar(has_next ? j + 3 : 1, 6, j, k, complete);
       }
     }
     ProfScope ps(ctx, K_SCALE, 16.0 * n);
@@ -434,8 +448,12 @@ struct FastIcgs {
     launch_copy(ctx->stream, t->desc(), X.desc(), n_local);
   }
 
-  // projectAndNormalize(X, [C], B, [Q]).
-  int project_and_normalize(migmres_mv &X, migmres_mv &Q, double *C, int ldc, double *B, int ldb) {
+  // projectAndNormalize(X, [C], B, [Q]).  The reference keeps a copy of X (tmpX) to restart
+  // from when a dependency is found; when the caller can recompute X exactly (regen: the
+  // same deterministic SpMM that produced it, not counted as an operator application) no
+  // copy is made.
+  int project_and_normalize(migmres_mv &X, migmres_mv &Q, double *C, int ldc, double *B, int ldb,
+                            const std::function<void()> *regen = nullptr) {
     ++calls;
     const int k = X.ncols, L = Q.ncols;
     launch_state_reset(ctx->stream, st, slow->blk_tol, slow->sing_tol);
@@ -443,9 +461,8 @@ struct FastIcgs {
     if (k == 1) {  // blkOrtho1, then MvDot and MvScale
       tn(qd, L, xd, 1, R1, L);
       nn_then_tn(qd, L, R1, L, xd, 1, R2);
-      nn(qd, L, R2, L, xd, 1, true);
-      reduce_small(1);
-      launch_fb_scalar(ctx->stream, st, red, 4, 0, 1, 0);
+      nn(qd, L, R2, L, xd, 1, 1);
+      reduce_scalar(1, 4, 0, 1, 0);
       {
         ProfScope ps(ctx, K_SCALE, 16.0 * n_local);
         launch_scale_col(ctx->stream, xd, 0, st, n_local);
@@ -456,7 +473,7 @@ struct FastIcgs {
       B[0] = hst().B[0];
       return 1;
     }
-    save_input(X);
+    if (!regen) save_input(X);
     // blkOrtho: oldDot comes from the Gram block of [Q X]^T X when Q and X are adjacent
     const bool adjacent = Q.contiguous() && X.contiguous() && Q.ld == X.ld && X.base == Q.base + (long long)L * Q.ld;
     if (adjacent) {
@@ -470,17 +487,19 @@ struct FastIcgs {
     }
     launch_blk_old(ctx->stream, st, R1, L + k, L, k);
     nn_then_tn(qd, L, R1, L + k, xd, k, R2);
-    nn(qd, L, R2, L, xd, k, true);
-    reduce_small(k);
-    launch_fb_scalar(ctx->stream, st, red, 3, 0, k, 0);
+    nn(qd, L, R2, L, xd, k, 3);
+    reduce_scalar(k + 1, 3, 0, k, 0);
     launch_add_coef(ctx->stream, R1, L + k, R2, L, Cout, L, L, k);
-    find_basis(xd, k, 0);
+    find_basis(xd, k, 0, true);
     fetch(L, k);
     const IcgsState &s = hst();
     if (s.neg != 0.0) throw Error(MIGMRES_ESTATE, "ICGS: negative definiteness in inner product");
     if (s.dep != 0.0 || s.failed >= 0) {
       ++fallbacks;
-      restore_input(X);
+      if (regen)
+        (*regen)();
+      else
+        restore_input(X);
       const int rank = slow->blk_ortho_sing(X, Q, C, ldc, B, ldb);
       MIG_HIP(hipStreamSynchronize(ctx->stream));
       return rank;
@@ -930,8 +949,10 @@ struct Engine {
       subH.assign((size_t)lcl * k, 0.0);
       subH2.assign((size_t)k * k, 0.0);
       auto t0 = Clock::now();
+      // X = A V_prev again, bit for bit, if the device ICGS has to restart from its input
+      const std::function<void()> regen = [&] { crs_apply(*lp.A, *Vprev, *Vnext, 1.0, 0.0); };
       const int rank = S->use_fast && S->fast.supports(k)
-                           ? S->fast.project_and_normalize(*Vnext, *Q, subH.data(), lcl, subH2.data(), k)
+                           ? S->fast.project_and_normalize(*Vnext, *Q, subH.data(), lcl, subH2.data(), k, &regen)
                            : S->ortho.project_and_normalize(*Vnext, *Q, subH.data(), lcl, subH2.data(), k);
       S->t_ortho += since(t0);
       for (int j = 0; j < k; ++j) {
