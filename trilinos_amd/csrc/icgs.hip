@@ -400,55 +400,60 @@ __global__ __launch_bounds__(256, 2) void k_nn_tn(MvDesc Q, int L, const double 
   }
 }
 
-// Wide variant for k <= 8: one 1024-thread workgroup per CU stages 64-row chunks (512 B
-// per Q column per visit instead of 128 B: with 16-row chunks the Q stream alone, no
-// compute, fell from 6.4 TB/s at L = 64 to 3.7 TB/s at L = 200, tools/mb_nntn.hip).
-//   phase 1: wave w = (row block rb = w & 3, K quarter kq = w >> 2) forms a 16 x k partial
+// Wide variants for k <= 8 stage RW-row chunks (RW = 64: one 1024-thread workgroup per CU;
+// RW = 32: two 512-thread workgroups per CU), 256-512 B per Q column per visit instead of
+// 128 B: with 16-row chunks the Q stream alone, no compute, fell from 6.4 TB/s at L = 64 to
+// 3.7 TB/s at L = 200 (tools/mb_nntn.hip).
+//   phase 1: wave w = (row block rb = w % RB, K quarter kq = w / RB) forms a 16 x k partial
 //            of Qc C1; the 4 K quarters are summed in a fixed order by the X1 owners,
-//   X1:      wave w owns column w of the chunk's 64 rows (one 512-B load and store),
-//   phase 2: wave w accumulates Q tile w (16 columns) against X1 over the 64 rows.
-// LDS: Qs[Lp][65] | Xs[64][16] | red[16][NJ][64] | C1s[Lp][4 NJ]; 1-deep register prefetch.
-constexpr int NW_ROWS = 64, NW_LDQ = 65;
-
+//   X1:      thread t owns row t % RW of column t / RW (one load and one store per chunk),
+//   phase 2: wave w accumulates Q tiles w, w + NWAVE, ... (16 columns each) against X1.
+// LDS: Qs[Lp][RW + 1] | Xs[RW][16] | red[NWAVE][NJ][64] | C1s[Lp][4 NJ]; 1-deep register
+// prefetch of the next chunk.
+template <int RW>
 static size_t nw_lds_bytes(int L, int NJ) {
   const int Lp = (L + 15) & ~15;
-  return sizeof(double) * ((size_t)Lp * NW_LDQ + 64 * 16 + 16 * NJ * 64 + (size_t)Lp * 4 * NJ);
+  return sizeof(double) * ((size_t)Lp * (RW + 1) + RW * 16 + (RW / 4) * NJ * 64 + (size_t)Lp * 4 * NJ);
 }
 
-template <int NM, int NJ>
-__global__ __launch_bounds__(1024, 1) void k_nn_tn_w(MvDesc Q, int L, const double *__restrict__ C1, int ldc,
+template <int RW, int NM, int NJ>
+__global__ __launch_bounds__(16 * RW) void k_nn_tn_w(MvDesc Q, int L, const double *__restrict__ C1, int ldc,
                                                      MvDesc X, int k, int nrows, double *__restrict__ partial,
                                                      double *__restrict__ sink) {
+  constexpr int NTH = 16 * RW, NWAVE = NTH / 64, RB = RW / 16, LDQ = RW + 1, LPC = RW / 2;
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int Lp = (L + 15) & ~15;
   double *Qs = sm;
-  double *Xs = sm + (size_t)Lp * NW_LDQ;
-  double *red = Xs + 64 * 16;
-  double *C1s = red + 16 * NJ * 64;  // [Lp][4 NJ], zero past L and k
+  double *Xs = sm + (size_t)Lp * LDQ;
+  double *red = Xs + RW * 16;
+  double *C1s = red + NWAVE * NJ * 64;  // [Lp][4 NJ], zero past L and k
   const int t = threadIdx.x, w = t >> 6, l = t & 63, c = l & 15, g = l >> 4, n4 = l & 3;
-  const int rb = w & 3, kq = w >> 2;
-  for (int e = t; e < (Lp - L) * NW_LDQ; e += 1024) Qs[L * NW_LDQ + e] = 0.0;
-  for (int e = t; e < Lp * 4 * NJ; e += 1024) {
+  const int rb = w % RB, kq = w / RB;
+  for (int e = t; e < (Lp - L) * LDQ; e += NTH) Qs[L * LDQ + e] = 0.0;
+  for (int e = t; e < Lp * 4 * NJ; e += NTH) {
     const int i = e / (4 * NJ), j = e % (4 * NJ);
     C1s[e] = (i < L && j < k) ? C1[i + (long long)j * ldc] : 0.0;
   }
-  double acc2[NJ];
+  double acc2[(16 + NWAVE - 1) / NWAVE][NJ];
 #pragma unroll
-  for (int jg = 0; jg < NJ; ++jg) acc2[jg] = 0.0;
+  for (int m = 0; m < (16 + NWAVE - 1) / NWAVE; ++m)
+#pragma unroll
+    for (int jg = 0; jg < NJ; ++jg) acc2[m][jg] = 0.0;
 
-  // loader: column lcol + 32 m (clamped), rows 2 (t & 31) and + 1 of the 64-row chunk
-  const int lrow = 2 * (t & 31), lcol = t >> 5;
+  // loader: column lcol + 32 m (clamped), rows lrow, lrow + 1 of the chunk
+  const int lrow = 2 * (t % LPC), lcol = t / LPC;
   auto scol = [&](int m) { const int i = lcol + 32 * m; return i < L ? i : L - 1; };
   const double *qb = Q.base + lrow;
   const long long qld = Q.ld;
-  // X1 owner: row l of the chunk in column w (columns >= k store into the sink)
-  const bool xok_col = w < k;
-  const double *xsrc = colp_(X, xok_col ? w : k - 1);
-  double *xdst = colp_(X, xok_col ? w : k - 1);
-  const int xjg = (w >> 2) < NJ ? (w >> 2) : NJ - 1;
-  const int xo = 16 * (l & 3) + 4 * ((l >> 2) & 3) + (w & 3);  // D lane of (row l & 15, column w)
-  const int xrb = l >> 4;
-  const long long nchunks = (nrows + NW_ROWS - 1) / NW_ROWS;
+  // X1 owner: row xr of column xj (columns >= k store into the sink)
+  const int xr = t % RW, xj = t / RW;
+  const bool xok_col = xj < k;
+  const double *xsrc = colp_(X, xok_col ? xj : k - 1);
+  double *xdst = colp_(X, xok_col ? xj : k - 1);
+  const int xjg = (xj >> 2) < NJ ? (xj >> 2) : NJ - 1;
+  const int xr16 = xr & 15, xrb = xr >> 4;
+  const int xo = 16 * (xr16 & 3) + 4 * (xr16 >> 2) + (xj & 3);  // D lane of (row, column)
+  const long long nchunks = (nrows + RW - 1) / RW;
   const long long G = gridDim.x;
   auto clampc = [&](long long chunk) { return chunk < nchunks ? chunk : nchunks - 1; };
 
@@ -457,68 +462,81 @@ __global__ __launch_bounds__(1024, 1) void k_nn_tn_w(MvDesc Q, int L, const doub
   {
     const long long c0 = clampc(blockIdx.x);
 #pragma unroll
-    for (int m = 0; m < NM; ++m) p[m] = *(const d2 *)(qb + scol(m) * qld + c0 * NW_ROWS);
-    xv = xsrc[c0 * NW_ROWS + l];
+    for (int m = 0; m < NM; ++m) p[m] = *(const d2 *)(qb + scol(m) * qld + c0 * RW);
+    xv = xsrc[c0 * RW + xr];
   }
   for (long long ch = blockIdx.x; ch < nchunks; ch += G) {
-    const long long r0 = ch * NW_ROWS;
+    const long long r0 = ch * RW;
 #pragma unroll
     for (int m = 0; m < NM; ++m) {
-      Qs[scol(m) * NW_LDQ + lrow] = p[m].x;
-      Qs[scol(m) * NW_LDQ + lrow + 1] = p[m].y;
+      if (NT_DIAG_MASK & 4) {
+        Qs[scol(m) * LDQ + lrow] = p[m].x;
+        Qs[scol(m) * LDQ + lrow + 1] = p[m].y;
+      } else if (p[m].x == 12345.0) {
+        Qs[0] = p[m].y;
+      }
     }
     const double xcur = xv;
     lds_barrier();
     {
       const long long cn = clampc(ch + G);
 #pragma unroll
-      for (int m = 0; m < NM; ++m) p[m] = *(const d2 *)(qb + scol(m) * qld + cn * NW_ROWS);
-      xv = xsrc[cn * NW_ROWS + l];
+      for (int m = 0; m < NM; ++m) p[m] = *(const d2 *)(qb + scol(m) * qld + cn * RW);
+      if (NT_DIAG_MASK & 8) xv = xsrc[cn * RW + xr];
     }
     // phase 1: rows 16 rb .. 16 rb + 15, K steps s = kq + 4 m
     double a1[NJ];
 #pragma unroll
     for (int jg = 0; jg < NJ; ++jg) a1[jg] = 0.0;
 #pragma unroll
-    for (int m = 0; m < 16; ++m) {
+    for (int m = 0; m < ((NT_DIAG_MASK & 1) ? 16 : 0); ++m) {
       const int s = kq + 4 * m;
       if (4 * s < L) {
-        const double qa = Qs[(4 * s + g) * NW_LDQ + 16 * rb + c];
+        const double qa = Qs[(4 * s + g) * LDQ + 16 * rb + c];
 #pragma unroll
         for (int jg = 0; jg < NJ; ++jg) a1[jg] = mfma4(qa, C1s[(4 * s + g) * 4 * NJ + 4 * jg + n4], a1[jg]);
       }
     }
 #pragma unroll
-    for (int jg = 0; jg < NJ; ++jg) red[((kq * 4 + rb) * NJ + jg) * 64 + l] = a1[jg];
+    for (int jg = 0; jg < NJ; ++jg) red[((kq * RB + rb) * NJ + jg) * 64 + l] = a1[jg];
     lds_barrier();
     {
-      const double d = (red[((0 * 4 + xrb) * NJ + xjg) * 64 + xo] + red[((1 * 4 + xrb) * NJ + xjg) * 64 + xo]) +
-                       (red[((2 * 4 + xrb) * NJ + xjg) * 64 + xo] + red[((3 * 4 + xrb) * NJ + xjg) * 64 + xo]);
-      const bool ok = xok_col && ch < nchunks && r0 + l < nrows;
+      const double d = (red[((0 * RB + xrb) * NJ + xjg) * 64 + xo] + red[((1 * RB + xrb) * NJ + xjg) * 64 + xo]) +
+                       (red[((2 * RB + xrb) * NJ + xjg) * 64 + xo] + red[((3 * RB + xrb) * NJ + xjg) * 64 + xo]);
+      const bool ok = xok_col && ch < nchunks && r0 + xr < nrows;
       const double x1 = ok ? xcur - d : 0.0;
-      double *dst = ok ? xdst + r0 + l : sink + t;
-      *dst = x1;
-      Xs[l * 16 + w] = x1;
+      double *dst = ok ? xdst + r0 + xr : sink + (blockIdx.x * NTH + t);
+      if (NT_DIAG_MASK & 8) *dst = x1;
+      Xs[xr * 16 + xj] = x1;
     }
     lds_barrier();
-    // phase 2: tile w (Q columns 16 w .. 16 w + 15) against the 64 rows of X1
-    if (16 * w < L) {
+    // phase 2: tiles w, w + NWAVE, ... against the RW rows of X1
 #pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        const double qa = Qs[(16 * w + c) * NW_LDQ + 4 * s + g];
+    for (int mm = 0; mm < ((NT_DIAG_MASK & 2) ? (16 + NWAVE - 1) / NWAVE : 0); ++mm) {
+      const int tt = w + NWAVE * mm;
+      if (16 * tt < L) {
 #pragma unroll
-        for (int jg = 0; jg < NJ; ++jg) acc2[jg] = mfma4(qa, Xs[(4 * s + g) * 16 + 4 * jg + n4], acc2[jg]);
+        for (int s = 0; s < RW / 4; ++s) {
+          const double qa = Qs[(16 * tt + c) * LDQ + 4 * s + g];
+#pragma unroll
+          for (int jg = 0; jg < NJ; ++jg)
+            acc2[mm][jg] = mfma4(qa, Xs[(4 * s + g) * 16 + 4 * jg + n4], acc2[mm][jg]);
+        }
       }
     }
     lds_barrier();
   }
-  // partial (L x k) of this workgroup: tile w rows 16 w + 4 b + m
+  // partial (L x k) of this workgroup: tile tt rows 16 tt + 4 b + m
   double *out = partial + (long long)blockIdx.x * L * k;
-  const int i = 16 * w + 4 * ((l >> 2) & 3) + (l >> 4);
 #pragma unroll
-  for (int jg = 0; jg < NJ; ++jg) {
-    const int j = 4 * jg + n4;
-    if (16 * w < L && i < L && j < k) out[i + (long long)j * L] = acc2[jg];
+  for (int mm = 0; mm < (16 + NWAVE - 1) / NWAVE; ++mm) {
+    const int tt = w + NWAVE * mm;
+    const int i = 16 * tt + 4 * ((l >> 2) & 3) + (l >> 4);
+#pragma unroll
+    for (int jg = 0; jg < NJ; ++jg) {
+      const int j = 4 * jg + n4;
+      if (16 * tt < L && i < L && j < k) out[i + (long long)j * L] = acc2[mm][jg];
+    }
   }
 }
 
@@ -547,23 +565,31 @@ static nt_kernel_t nt_pick(int L, int k) {
   }
 }
 
-template <int NJ>
+template <int RW, int NJ>
 static nt_kernel_t nw_pick_nm(int L) {
   switch ((L + 31) >> 5) {
-    case 1: return k_nn_tn_w<1, NJ>;
-    case 2: return k_nn_tn_w<2, NJ>;
-    case 3: return k_nn_tn_w<3, NJ>;
-    case 4: return k_nn_tn_w<4, NJ>;
-    case 5: return k_nn_tn_w<5, NJ>;
-    case 6: return k_nn_tn_w<6, NJ>;
-    case 7: return k_nn_tn_w<7, NJ>;
-    default: return k_nn_tn_w<8, NJ>;
+    case 1: return k_nn_tn_w<RW, 1, NJ>;
+    case 2: return k_nn_tn_w<RW, 2, NJ>;
+    case 3: return k_nn_tn_w<RW, 3, NJ>;
+    case 4: return k_nn_tn_w<RW, 4, NJ>;
+    case 5: return k_nn_tn_w<RW, 5, NJ>;
+    case 6: return k_nn_tn_w<RW, 6, NJ>;
+    case 7: return k_nn_tn_w<RW, 7, NJ>;
+    default: return k_nn_tn_w<RW, 8, NJ>;
   }
 }
 
-// The wide variant wins from L = 64 on (4.6 vs 3.4 TB/s at L = 64 and 200, 256^3 k = 8);
-// below that one workgroup per CU cannot hide the per-chunk latency.
-static bool nw_ok(int L, int k) { return L >= 64 && k <= 8 && nw_lds_bytes(L, (k + 3) >> 2) <= 160 * 1024; }
+#ifndef NT_WIDE_RW
+#define NT_WIDE_RW 32
+#endif
+constexpr int NW_RW = NT_WIDE_RW;  // rows per chunk of the wide variant (32: 2 WGs/CU, 64: 1 WG/CU)
+constexpr int NW_WG_PER_CU = NW_RW == 32 ? 2 : 1;
+
+// The wide variant wins from L = 64 on (256^3, k = 8); below that the per-chunk latency
+// is not hidden.  It needs NW_WG_PER_CU workgroups' LDS to fit in 160 KiB.
+static bool nw_ok(int L, int k) {
+  return L >= 64 && k <= 8 && nw_lds_bytes<NW_RW>(L, (k + 3) >> 2) * NW_WG_PER_CU <= 160 * 1024;
+}
 
 static int cu_count() {
   static int cus = 0;
@@ -578,8 +604,9 @@ static int cu_count() {
 
 int nn_tn_blocks(int nrows, int L, int k) {
   if (nw_ok(L, k)) {
-    const long long nchunks = (nrows + NW_ROWS - 1) / NW_ROWS;
-    const long long b = cu_count() < nchunks ? cu_count() : nchunks;
+    const long long nchunks = (nrows + NW_RW - 1) / NW_RW;
+    const long long want = (long long)NW_WG_PER_CU * cu_count();
+    const long long b = want < nchunks ? want : nchunks;
     return b < 1 ? 1 : (int)b;
   }
   int per_cu = 0;
@@ -601,8 +628,8 @@ void launch_nn_tn(hipStream_t s, MvDesc Q, int L, const double *C1, int ldc, MvD
   if (Q.cols) throw Error(MIGMRES_EINVAL, "nn_tn: Q must be a contiguous column range");
   if (nw_ok(L, k)) {
     const int NJ = (k + 3) >> 2;
-    nt_kernel_t f = NJ == 1 ? nw_pick_nm<1>(L) : nw_pick_nm<2>(L);
-    const size_t lds = nw_lds_bytes(L, NJ);
+    nt_kernel_t f = NJ == 1 ? nw_pick_nm<NW_RW, 1>(L) : nw_pick_nm<NW_RW, 2>(L);
+    const size_t lds = nw_lds_bytes<NW_RW>(L, NJ);
     static bool attr_set[2][9] = {};
     const int nm = (L + 31) >> 5;
     if (!attr_set[NJ - 1][nm]) {
@@ -610,7 +637,7 @@ void launch_nn_tn(hipStream_t s, MvDesc Q, int L, const double *C1, int ldc, MvD
         throw Error(MIGMRES_EHIP, "nn_tn: cannot raise the dynamic LDS limit");
       attr_set[NJ - 1][nm] = true;
     }
-    hipLaunchKernelGGL(f, dim3(nblocks), dim3(1024), lds, s, Q, L, C1, ldc, X, k, nrows, partial, sink);
+    hipLaunchKernelGGL(f, dim3(nblocks), dim3(16 * NW_RW), lds, s, Q, L, C1, ldc, X, k, nrows, partial, sink);
   } else {
     hipLaunchKernelGGL(nt_pick(L, k), dim3(nblocks), dim3(256), nt_lds_bytes(L), s, Q, L, C1, ldc, X, k, nrows,
                        partial, sink);

@@ -300,7 +300,8 @@ struct FastIcgs {
     MIG_HIP(hipMalloc(&R2, sizeof(double) * (size_t)(lmax + k) * k));
     MIG_HIP(hipMalloc(&Cout, sizeof(double) * (size_t)(lmax + k) * k));
     MIG_HIP(hipMalloc(&red, sizeof(double) * 64));
-    MIG_HIP(hipMalloc(&sink, sizeof(double) * 256 * (size_t)nn_tn_blocks(nl, 16, 1)));
+    // any nn_tn grid: at most 2048 workgroup-slots of 1024 threads' worth of lanes
+    MIG_HIP(hipMalloc(&sink, sizeof(double) * 1024 * 2048));
     const size_t sbytes = sizeof(double) * ((size_t)(nl > 0 ? nl : 1) + 64);
     MIG_HIP(hipMalloc(&S, sbytes));
     MIG_HIP(hipMemset(S, 0, sbytes));  // zero padding row read by the row-pair kernels
