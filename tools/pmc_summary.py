@@ -1,20 +1,31 @@
 """Summarise rocprofv3 PMC passes (separate FETCH_SIZE and WRITE_SIZE runs of the same
-bench command) into profiles/pmc_summary.json: per kernel the mean counters per dispatch
-and the HBM traffic per launch, corrected as MI355X_MICROARCH.md "HBM" prescribes:
-bytes = (FETCH_SIZE + WRITE_SIZE) * 1024, with FETCH_SIZE doubled for kernels whose reads
-are 16-byte-per-lane streaming loads (gfx950 reports half of those).
+bench command) into profiles/pmc_summary.json: per kernel class the HBM traffic per launch,
+corrected as MI355X_MICROARCH.md "HBM" prescribes: bytes = (FETCH_SIZE + WRITE_SIZE) * 1024,
+with FETCH_SIZE doubled for kernels whose reads are 16-byte-per-lane streaming loads (gfx950
+reports half of those).  Template instantiations of one kernel (k_nn_tn_w<32, 7, 2>, ...)
+are pooled into their bench class: traffic per launch = total corrected bytes / launches,
+the same averaging bench.py uses for the achieved rate.
 
 usage: python tools/pmc_summary.py FETCH.csv WRITE.csv STATS.csv OUT.json
 """
 import csv
 import json
+import re
 import sys
 from collections import defaultdict
 
-# rocprof kernel name -> (bench kernel class, reads are 16-B/lane streams)
+# kernel base name -> (bench class, reads are 16-B/lane streams)
+#   spmm: CSR values/keys are 2-8 B per lane and X pairs 16 B -> left uncorrected
 KMAP = {"k_gemm_tn": ("gemm_tn", True), "k_gemm_nn": ("gemm_nn", True),
-        "k_gemm_nn_dot": ("gemm_nn_dot", True), "k_spmm": ("spmm", False),
-        "k_fb_a": ("findbasis", True), "k_fb_b": ("findbasis", True), "k_fb_c": ("findbasis", True)}
+        "k_gemm_nn_dot": ("gemm_nn_dot", True), "k_nn_tn": ("nn_tn", True), "k_nn_tn_w": ("nn_tn", True),
+        "k_spmm": ("spmm", False), "k_spmm_pair": ("spmm", False),
+        "k_fb_a": ("findbasis", True), "k_fb_a01": ("findbasis", True), "k_fb_b2": ("findbasis", True),
+        "k_fb_ca": ("findbasis", True)}
+
+
+def base(name):
+    m = re.search(r"migmres::(k_[a-z0-9_]+)", name) or re.search(r"\b(k_[a-z0-9_]+)", name)
+    return m.group(1) if m else name
 
 
 def load(path, counter):
@@ -31,19 +42,25 @@ def main(fetch_csv, write_csv, stats_csv, out_json):
     out = {"source": {"fetch": fetch_csv, "write": write_csv, "stats": stats_csv},
            "note": "FETCH_SIZE/WRITE_SIZE are KiB; fetch doubled for 16-B/lane streaming reads (gfx950)",
            "kernels": {}, "rocprof_kernels": {}}
+    pool = defaultdict(lambda: [0.0, 0])
     for name in sorted(set(fe) | set(wr)):
-        f = sum(fe[name]) / max(len(fe[name]), 1)
-        w = sum(wr[name]) / max(len(wr[name]), 1)
-        cls, wide = KMAP.get(name, (name, False))
+        nf, nw = len(fe[name]), len(wr[name])
+        f = sum(fe[name]) / max(nf, 1)
+        w = sum(wr[name]) / max(nw, 1)
+        b = base(name)
+        cls, wide = KMAP.get(b, (b, False))
         traffic = ((2.0 if wide else 1.0) * f + w) * 1024.0
         st = stats.get(name)
-        out["rocprof_kernels"][name] = {"dispatches": len(fe[name]), "fetch_kib_mean": f, "write_kib_mean": w,
+        out["rocprof_kernels"][name] = {"class": cls, "dispatches": nf, "fetch_kib_mean": f, "write_kib_mean": w,
                                         "fetch_corrected": wide, "traffic_bytes_per_launch": traffic,
                                         "avg_duration_ns": float(st["AverageNs"]) if st else None}
-        if name in ("k_gemm_tn", "k_gemm_nn", "k_gemm_nn_dot", "k_spmm"):
-            out["kernels"][cls] = {"traffic_bytes_per_launch": traffic, "rocprof_kernel": name}
+        if b in KMAP:
+            pool[cls][0] += traffic * nf
+            pool[cls][1] += nf
+    for cls, (tot, n) in pool.items():
+        out["kernels"][cls] = {"traffic_bytes_per_launch": tot / max(n, 1), "dispatches": n}
     json.dump(out, open(out_json, "w"), indent=1)
-    print(json.dumps(out["rocprof_kernels"], indent=1))
+    print(json.dumps(out["kernels"], indent=1))
 
 
 if __name__ == "__main__":
