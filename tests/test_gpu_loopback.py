@@ -1,0 +1,133 @@
+"""The N > 1 device path on one GPU: P ranks as P host threads in one process, each with
+its own context (stream, buffers) joined through the library's in-process loopback
+communicator ("MIGLOOP1" unique id) instead of RCCL, which refuses two ranks on one GPU.
+Everything above the transport runs as on P GPUs: crs_create's remote-id exchange, the
+import plans, the halo pack/exchange into the ghost block, the SpMM kernels' ghost columns
+(row-pair and row-per-thread kernels), the all-reduced inner products and the solver.
+
+Parity: distributed SpMM bit for bit against the oracle's emulation of Epetra on P ranks
+(the sorted local column order differs from P = 1); distributed solves against the oracle
+with the solver-history tolerance of test_gpu_solver.py."""
+
+import os
+import struct
+import threading
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _uid():
+    return b"MIGLOOP1" + struct.pack("<Q", int.from_bytes(os.urandom(8), "little")) + bytes(112)
+
+
+def run_ranks(P, fn):
+    """fn(comm) on P threads (ctypes releases the GIL in library calls); returns results by rank."""
+    import trilinos_amd as ta
+    uid = _uid()
+    out, errs = [None] * P, []
+
+    def body(r):
+        try:
+            comm = ta.Comm(device=0, rank=r, nranks=P, unique_id=uid)
+            out[r] = fn(comm)
+        except BaseException as e:  # pragma: no cover - reported below
+            import traceback
+            errs.append(traceback.format_exc())
+            raise
+
+    # daemon threads: a rank that fails leaves the others waiting in the loopback barrier
+    th = [threading.Thread(target=body, args=(r,), daemon=True) for r in range(P)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not errs, errs[0]
+    assert not any(t.is_alive() for t in th), "a rank did not finish (loopback wait)"
+    return out
+
+
+def _gen(kind, dims):
+    from oracle import epetra as oe
+    nx, ny, nz = dims
+    if kind == "Laplace3D":
+        return nx * ny * nz, lambda f, m: oe.laplace3d_rows(nx, ny, nz, f, m)
+    if kind == "Laplace2D":
+        return nx * ny, lambda f, m: oe.laplace2d_rows(nx, ny, f, m)
+    from tests.test_plans import random_rows
+    n = nx
+    return n, lambda f, m: random_rows(n, f, m, 41, per_row=ny)
+
+
+@pytest.mark.parametrize("kind,dims,k,P", [("Laplace3D", (16, 16, 16), 8, 2), ("Laplace2D", (37, 23, 1), 3, 3),
+                                           ("Laplace3D", (9, 7, 5), 5, 4), ("random", (601, 4, 1), 8, 2),
+                                           ("random", (500, 11, 1), 2, 3)])
+def test_distributed_spmm_bit_exact(kind, dims, k, P):
+    import trilinos_amd as ta
+    from oracle import epetra as oe
+    n, gen = _gen(kind, dims)
+    X, _ = oe.epetra_random_mv(13, n, k)
+    Yref = oe.DistCrs(gen, n, P).apply(X)
+
+    def rank_fn(comm):
+        first, nloc = ta.uniform_map(n, comm.nranks, comm.rank)
+        if kind == "random":
+            rp, gc, vv = gen(first, nloc)
+            A = ta.CrsMatrix(comm, n, rp, gc, vv)
+        else:
+            A = ta.CrsMatrix.galeri(comm, kind, *dims)
+        Xd = ta.MultiVector(comm, n, k)
+        Xd.upload(X[first:first + nloc])
+        Yd = ta.MultiVector(comm, n, k)
+        A.apply(Xd, Yd)
+        return first, Yd.download(), A.n_remote
+
+    res = run_ranks(P, rank_fn)
+    Y = np.zeros((n, k))
+    for first, y, _ in res:
+        Y[first:first + y.shape[0]] = y
+    assert sum(r[2] for r in res) > 0  # ghost columns were exercised
+    assert np.array_equal(Y, Yref)
+
+
+@pytest.mark.parametrize("kind,dims,k,nb,P", [("Laplace2D", (30, 30, 1), 2, 15, 2),
+                                              ("Laplace3D", (12, 12, 12), 8, 5, 3)])
+def test_distributed_solve_matches_oracle(kind, dims, k, nb, P):
+    import trilinos_amd as ta
+    from oracle import belos as ob, epetra as oe
+    from tests.test_gpu_solver import _hist_close
+    n, gen = _gen(kind, dims)
+    Aor = oe.DistCrs(gen, n, P)
+    Xe, _ = oe.epetra_random_mv(5, n, k)
+    Bh = Aor.apply(Xe)
+    params = {"Num Blocks": nb, "Block Size": k, "Maximum Iterations": 400, "Maximum Restarts": 20,
+              "Convergence Tolerance": 1e-8, "Orthogonalization": "ICGS"}
+    ref = ob.solve(Aor.apply, Bh, params)
+
+    def rank_fn(comm):
+        first, nloc = ta.uniform_map(n, comm.nranks, comm.rank)
+        A = ta.CrsMatrix.galeri(comm, kind, *dims)
+        B = ta.MultiVector(comm, n, k)
+        B.upload(Bh[first:first + nloc])
+        X = ta.MultiVector(comm, n, k)
+        X.put_scalar(0.0)
+        lp = ta.LinearProblem(A, X, B)
+        assert lp.setProblem()
+        sm = ta.BlockGmresSolMgr(lp, params)
+        ret = sm.solve()
+        return ret, sm.getNumIters(), sm.counters(), sm.residualHistory(), first, X.download()
+
+    res = run_ranks(P, rank_fn)
+    for ret, iters, c, h, _, _ in res:
+        assert (ret == ta.Converged) == ref["converged"]
+        assert iters == ref["iterations"]
+        assert c["restarts"] == ref["restarts"] and c["applies"] == ref["n_apply"]
+        assert c["explicit_checks"] == ref["n_explicit"]
+        _hist_close(h, ref["history"], ref["restarts"])
+    X = np.zeros((n, k))
+    for r in res:
+        X[r[4]:r[4] + r[5].shape[0]] = r[5]
+    rel = np.linalg.norm(Bh - Aor.apply(X), axis=0) / np.linalg.norm(Bh, axis=0)
+    assert rel.max() <= 1e-8 * 1.01

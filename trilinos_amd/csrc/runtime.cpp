@@ -2,6 +2,11 @@
 #include "runtime.h"
 
 #include <chrono>
+#include <algorithm>
+#include <mutex>
+#include <map>
+#include <deque>
+#include <condition_variable>
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
@@ -51,11 +56,129 @@ double *migmres_ctx::pinned(size_t n) {
   }
   return h_pinned;
 }
+// ------------------------------------------------------------------------------------
+// in-process loopback communicator (tests only)
+// ------------------------------------------------------------------------------------
+namespace migmres {
+struct LoopGroup {
+  int n = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  long long ar_gen = 0;
+  int ar_arrived = 0;
+  std::vector<std::vector<double>> ar_in;
+  std::vector<double> ar_out;
+  std::map<std::pair<int, int>, std::deque<std::vector<char>>> box;  // (src, dst) -> messages
+};
+}  // namespace migmres
+
+static std::mutex g_loop_mu;
+static std::map<unsigned long long, std::weak_ptr<LoopGroup>> g_loop_groups;
+
+static bool is_loop_uid(const unsigned char *uid) { return uid && std::memcmp(uid, "MIGLOOP1", 8) == 0; }
+
+static std::shared_ptr<LoopGroup> loop_join(const unsigned char *uid, int nranks) {
+  unsigned long long key = 0;
+  std::memcpy(&key, uid + 8, sizeof(key));
+  std::lock_guard<std::mutex> lk(g_loop_mu);
+  auto &w = g_loop_groups[key];
+  auto g = w.lock();
+  if (!g) {
+    g = std::make_shared<LoopGroup>();
+    g->n = nranks;
+    g->ar_in.resize((size_t)nranks);
+    w = g;
+  }
+  MIG_CHECK(g->n == nranks, "loopback group joined with a different rank count");
+  return g;
+}
+
+// Blocking sum / max all-reduce across the group's ranks (rank order, deterministic).
+static void loop_allreduce(migmres_ctx *c, double *d, size_t n, bool max) {
+  LoopGroup &g = *c->loop;
+  std::vector<double> v(n);
+  MIG_HIP(hipStreamSynchronize(c->stream));
+  MIG_HIP(hipMemcpy(v.data(), d, sizeof(double) * n, hipMemcpyDeviceToHost));
+  std::vector<double> out;
+  {
+    std::unique_lock<std::mutex> lk(g.mu);
+    const long long gen = g.ar_gen;
+    g.ar_in[(size_t)c->rank] = std::move(v);
+    if (++g.ar_arrived == g.n) {
+      std::vector<double> r = g.ar_in[0];
+      for (int q = 1; q < g.n; ++q) {
+        MIG_CHECK(g.ar_in[(size_t)q].size() == n, "loopback all-reduce size mismatch");
+        for (size_t i = 0; i < n; ++i)
+          r[i] = max ? std::max(r[i], g.ar_in[(size_t)q][i]) : r[i] + g.ar_in[(size_t)q][i];
+      }
+      g.ar_out = std::move(r);
+      g.ar_arrived = 0;
+      ++g.ar_gen;
+      g.cv.notify_all();
+    } else {
+      g.cv.wait(lk, [&] { return g.ar_gen != gen; });
+    }
+    out = g.ar_out;
+  }
+  MIG_HIP(hipMemcpy(d, out.data(), sizeof(double) * n, hipMemcpyHostToDevice));
+}
+
+void migmres_ctx::p2p_begin() {
+  p2p_sends.clear();
+  p2p_recvs.clear();
+  if (!loop) MIG_NCCL(ncclGroupStart());
+}
+void migmres_ctx::p2p_send(const void *buf, size_t bytes, int peer) {
+  if (loop)
+    p2p_sends.push_back({const_cast<void *>(buf), bytes, peer});
+  else
+    MIG_NCCL(ncclSend(buf, bytes, ncclChar, peer, comm, stream));
+}
+void migmres_ctx::p2p_recv(void *buf, size_t bytes, int peer) {
+  if (loop)
+    p2p_recvs.push_back({buf, bytes, peer});
+  else
+    MIG_NCCL(ncclRecv(buf, bytes, ncclChar, peer, comm, stream));
+}
+void migmres_ctx::p2p_end() {
+  if (!loop) {
+    MIG_NCCL(ncclGroupEnd());
+    return;
+  }
+  LoopGroup &g = *loop;
+  MIG_HIP(hipStreamSynchronize(stream));
+  for (auto &m : p2p_sends) {
+    std::vector<char> v(m.bytes);
+    if (m.bytes) MIG_HIP(hipMemcpy(v.data(), m.buf, m.bytes, hipMemcpyDeviceToHost));
+    std::lock_guard<std::mutex> lk(g.mu);
+    g.box[{rank, m.peer}].push_back(std::move(v));
+    g.cv.notify_all();
+  }
+  for (auto &m : p2p_recvs) {
+    std::vector<char> v;
+    {
+      std::unique_lock<std::mutex> lk(g.mu);
+      auto &q = g.box[{m.peer, rank}];
+      g.cv.wait(lk, [&] { return !q.empty(); });
+      v = std::move(q.front());
+      q.pop_front();
+    }
+    MIG_CHECK(v.size() == m.bytes, "loopback message size mismatch");
+    if (m.bytes) MIG_HIP(hipMemcpy(m.buf, v.data(), m.bytes, hipMemcpyHostToDevice));
+  }
+  p2p_sends.clear();
+  p2p_recvs.clear();
+}
+
 void migmres_ctx::allreduce(double *d, size_t n, bool max) {
   if (nranks == 1 || n == 0) return;
   auto t0 = std::chrono::steady_clock::now();
-  MIG_NCCL(ncclAllReduce(d, d, n, ncclDouble, max ? ncclMax : ncclSum, comm, stream));
-  MIG_HIP(hipStreamSynchronize(stream));
+  if (loop) {
+    loop_allreduce(this, d, n, max);
+  } else {
+    MIG_NCCL(ncclAllReduce(d, d, n, ncclDouble, max ? ncclMax : ncclSum, comm, stream));
+    MIG_HIP(hipStreamSynchronize(stream));
+  }
   comm_seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
 
@@ -170,6 +293,10 @@ void migmres_ctx::pool_trim() {
 
 void migmres_ctx::allreduce_async(double *d, size_t n) {
   if (nranks == 1 || n == 0) return;
+  if (loop) {
+    loop_allreduce(this, d, n, false);
+    return;
+  }
   MIG_NCCL(ncclAllReduce(d, d, n, ncclDouble, ncclSum, comm, stream));
 }
 
@@ -195,9 +322,13 @@ extern "C" int migmres_ctx_create(int device, int rank, int nranks, const unsign
       MIG_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
       if (nranks > 1) {
         MIG_CHECK(uid != nullptr, "unique id required for nranks > 1");
-        ncclUniqueId id;
-        std::memcpy(&id, uid, 128);
-        MIG_NCCL(ncclCommInitRank(&c->comm, nranks, id, rank));
+        if (is_loop_uid(uid)) {
+          c->loop = loop_join(uid, nranks);
+        } else {
+          ncclUniqueId id;
+          std::memcpy(&id, uid, 128);
+          MIG_NCCL(ncclCommInitRank(&c->comm, nranks, id, rank));
+        }
       }
     } catch (...) {
       delete c;
@@ -575,13 +706,12 @@ migmres_crs *crs_create(migmres_ctx *ctx, long long n_global, long long first, i
       MIG_HIP(hipMalloc(&d_give, sizeof(long long) * (total_give > 0 ? total_give : 1)));
       if (n_remote)
         MIG_HIP(hipMemcpy(d_req, p.remote_gids.data(), sizeof(long long) * n_remote, hipMemcpyHostToDevice));
-      MIG_NCCL(ncclGroupStart());
-      for (auto &nb : A->recv_nbrs)
-        MIG_NCCL(ncclSend(d_req + nb.offset, nb.count, ncclInt64, nb.pid, ctx->comm, ctx->stream));
+      ctx->p2p_begin();
+      for (auto &nb : A->recv_nbrs) ctx->p2p_send(d_req + nb.offset, sizeof(long long) * nb.count, nb.pid);
       for (int q = 0; q < P; ++q)
         if (give_cnt[(size_t)q] > 0)
-          MIG_NCCL(ncclRecv(d_give + give_off[(size_t)q], give_cnt[(size_t)q], ncclInt64, q, ctx->comm, ctx->stream));
-      MIG_NCCL(ncclGroupEnd());
+          ctx->p2p_recv(d_give + give_off[(size_t)q], sizeof(long long) * give_cnt[(size_t)q], q);
+      ctx->p2p_end();
       std::vector<long long> give((size_t)total_give);
       if (total_give)
         MIG_HIP(hipMemcpyAsync(give.data(), d_give, sizeof(long long) * total_give, hipMemcpyDeviceToHost, ctx->stream));
@@ -658,16 +788,14 @@ void crs_apply(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, double alpha,
     }
     auto t0 = std::chrono::steady_clock::now();
     launch_pack(c->stream, X.desc(), A.d_export, n_export, A.d_send, k);
-    MIG_NCCL(ncclGroupStart());
+    c->p2p_begin();
     for (auto &nb : A.send_nbrs)
       for (int col = 0; col < k; ++col)
-        MIG_NCCL(ncclSend(A.d_send + (size_t)col * n_export + nb.offset, nb.count, ncclDouble, nb.pid,
-                          c->comm, c->stream));
+        c->p2p_send(A.d_send + (size_t)col * n_export + nb.offset, sizeof(double) * nb.count, nb.pid);
     for (auto &nb : A.recv_nbrs)
       for (int col = 0; col < k; ++col)
-        MIG_NCCL(ncclRecv(A.d_ghost + (size_t)col * A.ldg + nb.offset, nb.count, ncclDouble, nb.pid,
-                          c->comm, c->stream));
-    MIG_NCCL(ncclGroupEnd());
+        c->p2p_recv(A.d_ghost + (size_t)col * A.ldg + nb.offset, sizeof(double) * nb.count, nb.pid);
+    c->p2p_end();
     c->comm_seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
   ProfScope ps(c, K_SPMM, 12.0 * A.nnz + 4.0 * (A.n_local + 1) + 8.0 * A.n_local * k * (beta == 0.0 ? 2.0 : 3.0));

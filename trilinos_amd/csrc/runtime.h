@@ -4,6 +4,7 @@
 
 #include <rccl/rccl.h>
 
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -16,6 +17,9 @@ enum KernelClass { K_SPMM = 0, K_GEMM_TN, K_REDUCE, K_GEMM_NN, K_COLDOT, K_AXPBY
 extern const char *kKernelClassNames[K_NUM_CLASSES];
 
 struct migmres_ctx;
+namespace migmres {
+struct LoopGroup;
+}
 struct ProfScope {
   migmres_ctx *c;
   int cls;
@@ -50,6 +54,21 @@ struct migmres_ctx {
   void pool_trim();
   hipStream_t stream = nullptr;
   ncclComm_t comm = nullptr;
+  // In-process multi-rank emulation for tests (all ranks' contexts in one process on one
+  // device, one host thread per rank; selected by a "MIGLOOP1" unique id): collectives and
+  // point-to-point messages go through host mailboxes instead of RCCL.  See runtime.cpp.
+  std::shared_ptr<migmres::LoopGroup> loop;
+  struct P2p {
+    void *buf;
+    size_t bytes;
+    int peer;
+  };
+  std::vector<P2p> p2p_sends, p2p_recvs;
+  // grouped point-to-point exchange (ncclGroupStart/Send/Recv/GroupEnd on the stream)
+  void p2p_begin();
+  void p2p_send(const void *buf, size_t bytes, int peer);
+  void p2p_recv(void *buf, size_t bytes, int peer);
+  void p2p_end();
   // device scratch: per-workgroup partials, reduced results, staged coefficients
   double *d_partial = nullptr;
   size_t partial_cap = 0;
