@@ -171,6 +171,11 @@ int migmres_mv_set_block(const migmres_mv *A, const int *idx, int n, migmres_mv 
 int migmres_icgs_project_normalize(migmres_mv *X, const migmres_mv *Q, double *C, int ldc,
                                    double *B, int ldb, int *rank);
 int migmres_icgs_normalize(migmres_mv *X, double *B, int ldb, int *rank);
+/* Belos::DGKSOrthoManager (belos/src/BelosDGKSOrthoManager.hpp:644-815 projectAndNormalize,
+ * 828-840 normalize), default parameters (536-556).  Same arguments as the ICGS pair. */
+int migmres_dgks_project_normalize(migmres_mv *X, const migmres_mv *Q, double *C, int ldc,
+                                   double *B, int ldb, int *rank);
+int migmres_dgks_normalize(migmres_mv *X, double *B, int ldb, int *rank);
 
 /* ---------------- solver manager (Belos::BlockGmresSolMgr) ---------------- */
 

@@ -386,3 +386,46 @@ def read_hb(path):
     vals = floats(start + ptrcrd + indcrd, start + ptrcrd + indcrd + valcrd)
     assert colptr.size == ncol + 1 and rowind.size == nnz and vals.size == nnz
     return nrow, colptr, rowind, vals, mxtype[1] == "S"
+
+
+def scscmv(colptr, rowind, vals, x, symmetric=False):
+    """y = A x for a CSC matrix, column by column (triutils/src/Trilinos_Util_scscmv.cpp:40-80):
+    y[rowind[i]] += val[i] * x[j] in stored order, plus the mirrored entry for symmetric
+    storage.  Returns y."""
+    n = colptr.size - 1
+    y = np.zeros(n)
+    for j in range(n):
+        for i in range(colptr[j], colptr[j + 1]):
+            r = rowind[i]
+            y[r] = y[r] + vals[i] * x[j]
+            if symmetric and r != j:
+                y[j] = y[j] + vals[i] * x[r]
+    return y
+
+
+def hb_problem(colptr, rowind, vals, symmetric=False):
+    """Belos::Util::createEpetraProblem on a Harwell-Boeing file without a right-hand side
+    (belos/epetra/src/BelosEpetraUtils.cpp:81-200 -> Trilinos_Util_read_hb.cpp:141-158):
+    xexact[i] = rand() / RAND_MAX from glibc's stream, b = scscmv(A, xexact).  Returns
+    (row generator for DistCrs, b, xexact); the rows' insertion order does not matter
+    (FillComplete sorts them)."""
+    n = colptr.size - 1
+    xexact = np.array(glibc_rand(n), dtype=np.float64) / 2147483647.0
+    b = scscmv(colptr, rowind, vals, xexact, symmetric)
+    rows = [[] for _ in range(n)]
+    for j in range(n):
+        for i in range(colptr[j], colptr[j + 1]):
+            rows[rowind[i]].append((j, vals[i]))
+            if symmetric and rowind[i] != j:
+                rows[j].append((rowind[i], vals[i]))
+
+    def gen(first, nloc):
+        rp, gc, vv = [0], [], []
+        for r in range(first, first + nloc):
+            for c, v in rows[r]:
+                gc.append(c)
+                vv.append(v)
+            rp.append(len(gc))
+        return np.array(rp, dtype=np.int64), np.array(gc, dtype=np.int64), np.array(vv)
+
+    return gen, b, xexact

@@ -47,7 +47,22 @@ def problem(kind, dims, k, seed):
     return A, A.apply(Xex)
 
 
+ORSIRR1_SRC = "/root/reference/packages/belos/epetra/example/BlockGmres/orsirr1.hb"
+
+
+def orsirr1_fixture():
+    """orsirr1.hb (1030 x 1030, 6858 nnz; the matrix of belos/epetra/test/BlockGmres/
+    test_bl_gmres_hb.cpp) as CSC arrays, so tests do not read /root/reference.  Data only:
+    the Harwell-Boeing file's column pointers, row indices and values."""
+    n, colptr, rowind, vals, sym = oe.read_hb(ORSIRR1_SRC)
+    np.savez_compressed(os.path.join(HERE, "orsirr1.npz"), n=n, colptr=colptr, rowind=rowind, vals=vals,
+                        symmetric=sym)
+    print("orsirr1", n, rowind.size)
+
+
 def main(names=None):
+    if not names or "orsirr1" in names:
+        orsirr1_fixture()
     for name, (kind, dims, k, seed, params) in CASES.items():
         if names and name not in names:
             continue

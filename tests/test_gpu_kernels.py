@@ -173,3 +173,25 @@ def test_icgs_project_normalize(comm):
     Xn = Xd.download()
     np.testing.assert_allclose(Xn.T @ Xn, np.eye(k), atol=1e-13)
     np.testing.assert_allclose(Q.T @ Xn, 0, atol=1e-13)
+
+
+@pytest.mark.parametrize("k,near_dep", [(8, False), (1, False), (1, True), (4, True)])
+def test_dgks_project_normalize(comm, k, near_dep):
+    """DGKSOrthoManager::projectAndNormalize against the oracle.  near_dep makes X lie mostly
+    in span(Q), so the DGKS re-orthogonalisation criterion fires (and for k = 1 the second
+    blkOrtho1 pass runs)."""
+    import trilinos_amd as ta
+    from oracle.dgks import DGKS
+    rng = np.random.default_rng(17 + k)
+    n, L = 3000, 24
+    Q, _ = np.linalg.qr(rng.standard_normal((n, L)))
+    X = Q @ rng.standard_normal((L, k)) + (1e-3 if near_dep else 1.0) * rng.standard_normal((n, k))
+    Qd, Xd = _upload(ta, comm, Q), _upload(ta, comm, X)
+    rank, C, B = ta.DGKSOrthoManager().projectAndNormalize(Xd, Qd)
+    Xo = X.copy()
+    Co, Bo = np.zeros((L, k)), np.zeros((k, k))
+    r_or = DGKS().project_and_normalize(Xo, Q, Co, Bo)
+    assert rank == r_or == k
+    np.testing.assert_allclose(C, Co, rtol=1e-10, atol=1e-12)
+    np.testing.assert_allclose(B, Bo, rtol=1e-10, atol=1e-12)
+    np.testing.assert_allclose(Xd.download(), Xo, rtol=1e-9, atol=1e-11)

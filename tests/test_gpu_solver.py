@@ -218,3 +218,51 @@ def test_dependent_blocks_blkorthosing(comm):
     assert c["explicit_checks"] == ref["n_explicit"]
     assert c["blk_ortho_sing"] == ref["blk_ortho_sing"]
     _hist_close(sm.residualHistory(), ref["history"], ref["restarts"])
+
+
+@pytest.mark.parametrize("kind,dims,k,nb,seed", [("Laplace3D", (16, 16, 16), 8, 6, 3),
+                                                 ("Laplace2D", (40, 25, 1), 3, 20, 2),
+                                                 ("Laplace2D", (30, 30, 1), 1, 20, 1)])
+def test_dgks_solves_match_oracle(comm, kind, dims, k, nb, seed):
+    """The reference's default orthogonalization on the device path (blkOrtho + the DGKS
+    findBasis with its conditional second projection; k = 1 takes the host-driven DGKS
+    blkOrtho1) against the oracle's DGKSOrthoManager restatement."""
+    from oracle import belos as ob, epetra as oe
+    params = {"Num Blocks": nb, "Block Size": k, "Maximum Iterations": 2000, "Maximum Restarts": 30,
+              "Convergence Tolerance": 1e-8, "Orthogonalization": "DGKS"}
+    sm, ret, X, B, Xex = _device_solve(comm, kind, dims, k, seed, params)
+    n, gen = _gen(kind, dims)
+    A = oe.DistCrs(gen, n, 1)
+    ref = ob.solve(A.apply, A.apply(Xex), params)
+    c = sm.counters()
+    assert sm.getNumIters() == ref["iterations"]
+    assert c["restarts"] == ref["restarts"] and c["applies"] == ref["n_apply"]
+    assert c["explicit_checks"] == ref["n_explicit"]
+    _hist_close(sm.residualHistory(), ref["history"], ref["restarts"])
+
+
+def test_dgks_orsirr1_reference_run(comm):
+    """test_bl_gmres_hb.cpp on orsirr1.hb with the default DGKS: the reference run recorded
+    209 iterations and an actual relative residual of 9.94786e-06."""
+    import trilinos_amd as ta
+    from oracle import belos as ob, epetra as oe
+    from tests.test_oracle_pins import orsirr1_problem
+    n, gen, b, _ = orsirr1_problem()
+    rp, gc, vv = gen(0, n)
+    A = ta.CrsMatrix(comm, n, rp, gc, vv)
+    B = ta.MultiVector(comm, n, 1)
+    B.upload(b[:, None])
+    X = ta.MultiVector(comm, n, 1)
+    X.put_scalar(0.0)
+    lp = ta.LinearProblem(A, X, B)
+    assert lp.setProblem()
+    params = {"Num Blocks": n - 1, "Block Size": 1, "Maximum Iterations": n - 1, "Maximum Restarts": 15,
+              "Convergence Tolerance": 1e-5}  # Orthogonalization: the default, "DGKS"
+    sm = ta.BlockGmresSolMgr(lp, params)
+    assert sm.solve() == ta.Converged
+    assert sm.getNumIters() == 209
+    Aor = oe.DistCrs(gen, n, 1)
+    rel = np.linalg.norm(b - Aor.apply(X.download())[:, 0]) / np.linalg.norm(b)
+    assert f"{rel:.5e}" == "9.94786e-06"
+    ref = ob.solve(Aor.apply, b[:, None], dict(params, Orthogonalization="DGKS"))
+    _hist_close(sm.residualHistory(), ref["history"], ref["restarts"])

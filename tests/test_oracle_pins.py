@@ -83,3 +83,27 @@ def test_reference_run_64cube_icgs():
     assert res["n_explicit"] == 61
     rel = np.linalg.norm(B - A.apply(res["X"]), axis=0) / np.linalg.norm(B, axis=0)
     assert f"{rel.min():.1e}" == "3.5e-10" and f"{rel.max():.1e}" == "9.9e-09"
+
+
+def orsirr1_problem():
+    """test_bl_gmres_hb.cpp's problem: orsirr1.hb, xexact = rand()/RAND_MAX, b = A xexact by
+    the CSC product (Trilinos_Util_read_hb.cpp:141-158).  From the committed fixture."""
+    import os
+    f = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "orsirr1.npz"))
+    n = int(f["n"])
+    gen, b, xexact = oe.hb_problem(f["colptr"], f["rowind"], f["vals"], bool(f["symmetric"]))
+    return n, gen, b, xexact
+
+
+def test_reference_run_orsirr1_dgks():
+    """`test_bl_gmres_hb` (BlockGmres, k = 1, default DGKS, tol 1e-5,
+    Num Blocks = Max Iters = n - 1, 15 restarts) on orsirr1.hb: 209 iterations, actual
+    relative residual printed as 9.94786e-06."""
+    n, gen, b, _ = orsirr1_problem()
+    A = oe.DistCrs(gen, n, 1)
+    res = ob.solve(A.apply, b[:, None], {"Num Blocks": n - 1, "Block Size": 1, "Maximum Iterations": n - 1,
+                                          "Maximum Restarts": 15, "Convergence Tolerance": 1e-5,
+                                          "Orthogonalization": "DGKS"})
+    assert res["converged"] and res["iterations"] == 209
+    rel = np.linalg.norm(b - A.apply(res["X"])[:, 0]) / np.linalg.norm(b)
+    assert f"{rel:g}" == "9.94786e-06"

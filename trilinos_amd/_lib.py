@@ -67,6 +67,8 @@ _SIGS = {
     "migmres_mv_set_block": [vp, P(i32), i32, vp],
     "migmres_icgs_project_normalize": [vp, vp, P(f64), i32, P(f64), i32, P(i32)],
     "migmres_icgs_normalize": [vp, P(f64), i32, P(i32)],
+    "migmres_dgks_project_normalize": [vp, vp, P(f64), i32, P(f64), i32, P(i32)],
+    "migmres_dgks_normalize": [vp, P(f64), i32, P(i32)],
     "migmres_solver_create": [vp, P(vp)],
     "migmres_solver_destroy": [vp],
     "migmres_solver_set_int": [vp, C.c_char_p, i64],

@@ -4,6 +4,7 @@
                      Epetra specialisation belos/epetra/src/BelosEpetraAdapter.hpp:447-1064)
   OperatorTraits     Belos::OperatorTraits<double,MV,OP> (belos/src/BelosOperatorTraits.hpp:108-155)
   ICGSOrthoManager   Belos::ICGSOrthoManager (belos/src/BelosICGSOrthoManager.hpp:646-839)
+  DGKSOrthoManager   Belos::DGKSOrthoManager (belos/src/BelosDGKSOrthoManager.hpp:644-840)
   LinearProblem      Belos::LinearProblem (belos/src/BelosLinearProblem.hpp)
   BlockGmresSolMgr   Belos::BlockGmresSolMgr (belos/src/BelosBlockGmresSolMgr.hpp)
 
@@ -135,20 +136,28 @@ class ICGSOrthoManager:
     """projectAndNormalize / normalize with the reference defaults (2 passes,
     blk_tol = 10 sqrt(eps), sing_tol = 10 eps)."""
 
+    _pn, _n = "migmres_icgs_project_normalize", "migmres_icgs_normalize"
+
     def projectAndNormalize(self, X, Q):
         """Returns (rank, C, B) with C = (Q.ncols x X.ncols), B = (X.ncols x X.ncols)."""
         Cm = np.zeros((Q.ncols, X.ncols), order="F")
         Bm = np.zeros((X.ncols, X.ncols), order="F")
         r = C.c_int()
-        call("migmres_icgs_project_normalize", X.h, Q.h, dptr(Cm), max(Q.ncols, 1), dptr(Bm),
-             max(X.ncols, 1), C.byref(r))
+        call(self._pn, X.h, Q.h, dptr(Cm), max(Q.ncols, 1), dptr(Bm), max(X.ncols, 1), C.byref(r))
         return r.value, Cm, Bm
 
     def normalize(self, X):
         Bm = np.zeros((X.ncols, X.ncols), order="F")
         r = C.c_int()
-        call("migmres_icgs_normalize", X.h, dptr(Bm), max(X.ncols, 1), C.byref(r))
+        call(self._n, X.h, dptr(Bm), max(X.ncols, 1), C.byref(r))
         return r.value, Bm
+
+
+class DGKSOrthoManager(ICGSOrthoManager):
+    """Belos::DGKSOrthoManager (belos/src/BelosDGKSOrthoManager.hpp) with its defaults
+    (2 passes, blk_tol = 10 sqrt(eps), dep_tol = 1/sqrt(2), sing_tol = 10 eps)."""
+
+    _pn, _n = "migmres_dgks_project_normalize", "migmres_dgks_normalize"
 
 
 class LinearProblem:
@@ -188,9 +197,8 @@ DEFAULT_PARAMETERS = {
 class BlockGmresSolMgr:
     """Belos::BlockGmresSolMgr over the device solver.
 
-    Parameters use the reference ParameterList names.  Only the "ICGS"
-    orthogonalization is implemented on the device path; setting "DGKS" or "IMGS"
-    raises at solve() (the reference default "DGKS" is listed in SURVEY.md 8(f) as next).
+    Parameters use the reference ParameterList names.  "ICGS" and "DGKS" (the reference
+    default) orthogonalization run on the device path; "IMGS" raises at solve().
     """
 
     def __init__(self, problem=None, params=None):
@@ -225,7 +233,7 @@ class BlockGmresSolMgr:
         elif name in _STRING_PARAMS:
             if name == "Orthogonalization" and v not in ("DGKS", "ICGS", "IMGS"):
                 raise ValueError('"Orthogonalization" must be either "DGKS", "ICGS", or "IMGS".')
-            if name == "Orthogonalization" and v != "ICGS":
+            if name == "Orthogonalization" and v not in ("ICGS", "DGKS"):
                 return  # validated at solve()
             call("migmres_solver_set_string", self.h, n, str(v).encode())
 
@@ -256,8 +264,8 @@ class BlockGmresSolMgr:
         if self.problem is None or not self.problem.isProblemSet():
             raise RuntimeError("BlockGmresSolMgr::solve(): Linear problem is not ready, "
                                "setProblem() has not been called.")
-        if self.params["Orthogonalization"] != "ICGS":
-            raise NotImplementedError('device Block GMRES implements "Orthogonalization" = "ICGS"')
+        if self.params["Orthogonalization"] not in ("ICGS", "DGKS"):
+            raise NotImplementedError('device Block GMRES implements "Orthogonalization" = "ICGS" and "DGKS"')
         self._ensure()
         conv = C.c_int()
         call("migmres_solver_solve", self.h, self.problem.A.h, self.problem.X.h,

@@ -13,7 +13,8 @@ struct IcgsState {
   double blk_old[16];
   double blk_tol, sing_tol, dep, neg;
   int failed;  // first findBasis column found dependent, -1 if none
-  int pad_;
+  int dgks;    // 1: DGKSOrthoManager findBasis (second projection only under dep_tol)
+  double dep_tol;
 };
 
 int icgs_blocks(int nrows);
@@ -43,7 +44,8 @@ void launch_reduce_scalar(hipStream_t s, const double *partial, int nblocks, int
                           int stage, int j, int k, int complete);
 void launch_fb_scalar(hipStream_t s, IcgsState *st, const double *red, int stage, int j, int k, int complete);
 void launch_blk_old(hipStream_t s, IcgsState *st, const double *G, int ldg, int L, int k);
-void launch_state_reset(hipStream_t s, IcgsState *st, double blk_tol, double sing_tol);
+void launch_state_reset(hipStream_t s, IcgsState *st, double blk_tol, double sing_tol, int dgks = 0,
+                        double dep_tol = 0.0);
 void launch_add_coef(hipStream_t s, const double *C1, int ld1, const double *C2, int ld2, double *out, int ldo,
                      int L, int k);
 

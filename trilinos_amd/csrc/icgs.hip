@@ -767,11 +767,13 @@ __global__ __launch_bounds__(256) void k_fb_a01(MvDesc X, int nrows, double *__r
 }
 
 // (b2) normalise column j-1 in place (x * inv[j-1]); x1 = X_j - sum_i X_i P_i -> S;
-// partials <X_i, x1> (i < j), X_{j-1} taken normalised.
+// partials <X_i, x1> (i < j) and <x1, x1> (index j, the DGKS re-orthogonalisation test),
+// X_{j-1} taken normalised.
 __global__ __launch_bounds__(256) void k_fb_b2(MvDesc X, int j, const IcgsState *__restrict__ st,
                                                double *__restrict__ S, int nrows, double *__restrict__ partial) {
-  double v[16];
+  double v[17];
   double P[16];
+  v[16] = 0.0;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     v[i] = 0.0;
@@ -809,8 +811,11 @@ __global__ __launch_bounds__(256) void k_fb_b2(MvDesc X, int j, const IcgsState 
 #pragma unroll
     for (int i = 0; i < 16; ++i)
       if (i < j) v[i] += q[i].x * a0 + q[i].y * a1;
+#pragma unroll
+    for (int i = 0; i < 17; ++i)
+      if (i == j) v[i] += a0 * a0 + a1 * a1;
   }
-  block_reduce_store<16>(v, j, partial);
+  block_reduce_store<17>(v, j + 1, partial);
 }
 
 // (ca) x2 = S - sum_i X_i P2_i -> X_j (not normalised); partials
@@ -931,9 +936,13 @@ __device__ void fb_scalar_body(IcgsState *st, const double *red, int stage, int 
       st->B[0] = diag;
     }
   } else if (stage == 1) {
+    // red[0..j-1] = <X_i, x1>, red[j] = <x1, x1>.  DGKS (BelosDGKSOrthoManager.hpp:1086-1119)
+    // projects a second time only if sqrt|<x1,x1>| < dep_tol sqrt|oldDot|; otherwise the
+    // second update runs with zero coefficients, which leaves x1 unchanged bit for bit.
+    const bool reorth = !st->dgks || sqrt(fabs(red[j])) < st->dep_tol * sqrt(fabs(st->oldDot[j]));
     for (int i = 0; i < j; ++i) {
-      st->P2[i] = red[i];
-      st->prod[i] = st->prod[i] + red[i];
+      st->P2[i] = reorth ? red[i] : 0.0;
+      if (reorth) st->prod[i] = st->prod[i] + red[i];
     }
   } else if (stage == 2) {
     const double nd = red[0];
@@ -1018,8 +1027,10 @@ __global__ void k_blk_old(IcgsState *st, const double *__restrict__ G, int ldg, 
   for (int c = 0; c < k; ++c) st->blk_old[c] = G[(L + c) + (long long)c * ldg];
 }
 
-__global__ void k_state_reset(IcgsState *st, double blk_tol, double sing_tol) {
+__global__ void k_state_reset(IcgsState *st, double blk_tol, double sing_tol, int dgks, double dep_tol) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  st->dgks = dgks;
+  st->dep_tol = dep_tol;
   st->failed = -1;
   st->dep = 0.0;
   st->neg = 0.0;
@@ -1081,8 +1092,8 @@ void launch_blk_old(hipStream_t s, IcgsState *st, const double *G, int ldg, int 
   k_blk_old<<<1, 64, 0, s>>>(st, G, ldg, L, k);
   LAUNCH_CHECK_();
 }
-void launch_state_reset(hipStream_t s, IcgsState *st, double blk_tol, double sing_tol) {
-  k_state_reset<<<1, 64, 0, s>>>(st, blk_tol, sing_tol);
+void launch_state_reset(hipStream_t s, IcgsState *st, double blk_tol, double sing_tol, int dgks, double dep_tol) {
+  k_state_reset<<<1, 64, 0, s>>>(st, blk_tol, sing_tol, dgks, dep_tol);
   LAUNCH_CHECK_();
 }
 void launch_add_coef(hipStream_t s, const double *C1, int ld1, const double *C2, int ld2, double *out, int ldo,

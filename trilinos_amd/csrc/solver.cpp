@@ -66,10 +66,16 @@ const double kEps = std::numeric_limits<double>::epsilon();
 // ICGS orthogonalisation manager (max_ortho_steps = 2, blk_tol = 10 sqrt(eps),
 // sing_tol = 10 eps: BelosICGSOrthoManager.hpp:561-573)
 // ------------------------------------------------------------------------------------
+// With dgks = true the same object is Belos::DGKSOrthoManager (BelosDGKSOrthoManager.hpp,
+// defaults 536-556: 2 passes, blk_tol = 10 sqrt(eps), dep_tol = 1/sqrt(2), sing_tol = 10 eps):
+// the same projectAndNormalize / blkOrtho, but blkOrtho1, findBasis and blkOrthoSing
+// re-orthogonalise only when the first pass lost too much (the dep_tol criterion).
 struct Icgs {
   int steps = 2;
   double blk_tol = 10.0 * std::sqrt(kEps);
   double sing_tol = 10.0 * kEps;
+  bool dgks = false;
+  double dep_tol = 1.0 / std::sqrt(2.0);
   unsigned int seed = 12345u;  // MvRandom stream for rank-deficiency fallbacks
   long long sing_count = 0;
 
@@ -103,12 +109,23 @@ struct Icgs {
 
   int normalize(migmres_mv &X, double *B, int ldb) { return find_basis(X, B, ldb, true); }
 
-  // blkOrtho1 (BelosICGSOrthoManager.hpp:1231-1322)
+  // blkOrtho1 (BelosICGSOrthoManager.hpp:1231-1322; DGKS: BelosDGKSOrthoManager.hpp:1245-1321)
   void blk_ortho1(migmres_mv &X, migmres_mv &Q, double *C, int ldc) {
     const int L = Q.ncols, k = X.ncols;
+    double old_dot = 0.0;
+    if (dgks) old_dot = dot1(X, X);
     mv_trans_mv(1.0, Q, X, C, ldc);
     mv_times_mat_add_mv(-1.0, Q, C, ldc, 1.0, X);
     std::vector<double> C2((size_t)L * k);
+    if (dgks) {
+      const double new_dot = dot1(X, X);
+      if (std::sqrt(std::fabs(new_dot)) < dep_tol * std::sqrt(std::fabs(old_dot))) {
+        mv_trans_mv(1.0, Q, X, C2.data(), L);
+        for (int i = 0; i < L; ++i) C[i] += C2[(size_t)i];
+        mv_times_mat_add_mv(-1.0, Q, C2.data(), L, 1.0, X);
+      }
+      return;
+    }
     for (int s = 1; s < steps; ++s) {
       mv_trans_mv(1.0, Q, X, C2.data(), L);
       for (int j = 0; j < k; ++j)
@@ -147,6 +164,10 @@ struct Icgs {
       if (j > 0) {
         P2.assign((size_t)j, 0.0);
         for (int s = 0; s < steps; ++s) {
+          if (dgks && s > 0) {  // BelosDGKSOrthoManager.hpp:1086-1119
+            const double nd = dot1(*Xj, *Xj);
+            if (!(std::sqrt(std::fabs(nd)) < dep_tol * std::sqrt(std::fabs(old_dot)))) break;
+          }
           mv_trans_mv(1.0, *prevX, *Xj, P2.data(), j);
           mv_times_mat_add_mv(-1.0, *prevX, P2.data(), j, 1.0, *Xj);
           for (int i = 0; i < j; ++i) product[(size_t)i] = (s == 0) ? P2[(size_t)i] : product[(size_t)i] + P2[(size_t)i];
@@ -176,7 +197,7 @@ struct Icgs {
         return j;
       }
       const double diag = std::sqrt(std::fabs(new_dot));
-      mv_scale(*Xj, 1.0 / diag);
+      if (!dgks || std::fabs(diag) > 0.0) mv_scale(*Xj, 1.0 / diag);
       B[j + (size_t)j * ldb] = add_vec ? 0.0 : diag;
       if (!add_vec)
         for (int i = 0; i < j; ++i) B[i + (size_t)j * ldb] = product[(size_t)i];
@@ -205,7 +226,12 @@ struct Icgs {
         mv_trans_mv(1.0, *Qs[i], *Xj, col, q);
         mv_times_mat_add_mv(-1.0, *Qs[i], col, q, 1.0, *Xj);
       }
-      for (int s = 1; s < steps; ++s) {
+      bool second = true;
+      if (dgks) {  // BelosDGKSOrthoManager.hpp:1590-1625: re-orthogonalise on |new| < |old dep_tol|
+        new_dot = dot1(*Xj, *Xj);
+        second = std::fabs(new_dot) < std::fabs(old_dot * dep_tol);
+      }
+      for (int s = 1; s < steps && second; ++s) {
         for (int i = 0; i < nq; ++i) {
           const int q = Qs[i]->ncols;
           double *col = Cs[i] + (size_t)j * lds[i];
@@ -213,6 +239,7 @@ struct Icgs {
           for (int r = 0; r < q; ++r) col[r] += c2[(size_t)r];
           mv_times_mat_add_mv(-1.0, *Qs[i], c2.data(), q, 1.0, *Xj);
         }
+        if (dgks) new_dot = dot1(*Xj, *Xj);
       }
       const bool dep = std::fabs(new_dot) < std::fabs(old_dot * sing_tol);
       if (!dep) {
@@ -416,7 +443,7 @@ struct FastIcgs {
           ProfScope ps(ctx, K_FB, 8.0 * n * (j + 3));
           launch_fb_b2(ctx->stream, X, j, st, S, n_local, partial, nblk_ic);
         }
-        reduce_scalar(j, 1, j, k, complete);
+        reduce_scalar(j + 1, 1, j, k, complete);
         const int has_next = j + 1 < k;
         {
           ProfScope ps(ctx, K_FB, 8.0 * n * (j + 3 + has_next));
@@ -455,9 +482,11 @@ struct FastIcgs {
   // copy is made.
   int project_and_normalize(migmres_mv &X, migmres_mv &Q, double *C, int ldc, double *B, int ldb,
                             const std::function<void()> *regen = nullptr) {
-    ++calls;
     const int k = X.ncols, L = Q.ncols;
-    launch_state_reset(ctx->stream, st, slow->blk_tol, slow->sing_tol);
+    // DGKS blkOrtho1 decides its second pass on a dot product between the passes: host path
+    if (k == 1 && slow->dgks) return slow->project_and_normalize(X, Q, C, ldc, B, ldb);
+    ++calls;
+    launch_state_reset(ctx->stream, st, slow->blk_tol, slow->sing_tol, slow->dgks ? 1 : 0, slow->dep_tol);
     const MvDesc xd = X.desc(), qd = Q.desc();
     if (k == 1) {  // blkOrtho1, then MvDot and MvScale
       tn(qd, L, xd, 1, R1, L);
@@ -516,7 +545,7 @@ struct FastIcgs {
   int normalize(migmres_mv &X, double *B, int ldb) {
     ++calls;
     const int k = X.ncols;
-    launch_state_reset(ctx->stream, st, slow->blk_tol, slow->sing_tol);
+    launch_state_reset(ctx->stream, st, slow->blk_tol, slow->sing_tol, slow->dgks ? 1 : 0, slow->dep_tol);
     save_input(X);
     find_basis(X.desc(), k, 1);
     fetch(0, k);
@@ -1011,6 +1040,7 @@ struct Engine {
         mv_assign(*r0v, *V0);
       }
       std::vector<double> z0((size_t)block * block, 0.0);
+      S->ortho.dgks = S->p.ortho == "DGKS";
       if (S->use_fast && S->fast.supports(block)) {
         S->fast.slow = &S->ortho;
         S->fast.setup(lp.X->ctx, lp.X->n_global, lp.X->n_local, block, it.sd);
@@ -1142,7 +1172,7 @@ extern "C" int migmres_solver_set_string(migmres_solver *s, const char *name, co
     if (n == "Orthogonalization") {
       MIG_CHECK(val == "DGKS" || val == "ICGS" || val == "IMGS",
                 "\"Orthogonalization\" must be either \"DGKS\", \"ICGS\", or \"IMGS\"");
-      MIG_CHECK(val == "ICGS", "only \"ICGS\" is implemented on the device path");
+      MIG_CHECK(val == "ICGS" || val == "DGKS", "\"IMGS\" is not implemented on the device path");
       s->p.ortho = val;
     } else if (n == "Implicit Residual Scaling") {
       MIG_CHECK(val == "Norm of Preconditioned Initial Residual", "only the default implicit scaling is supported");
@@ -1156,7 +1186,7 @@ extern "C" int migmres_solver_solve(migmres_solver *s, migmres_crs *A, migmres_m
                                     const migmres_mv *B, int *converged) {
   return guard([&] {
     MIG_CHECK(s && A && X && B, "bad solve arguments");
-    MIG_CHECK(s->p.ortho == "ICGS", "set \"Orthogonalization\" to \"ICGS\"");
+    MIG_CHECK(s->p.ortho == "ICGS" || s->p.ortho == "DGKS", "\"Orthogonalization\" must be \"ICGS\" or \"DGKS\"");
     MIG_CHECK(X->ncols == B->ncols && X->n_local == A->n_local && B->n_local == A->n_local,
               "LinearProblem: inconsistent X/B/A shapes");
     s->history.clear();
@@ -1209,6 +1239,25 @@ extern "C" int migmres_solver_timers(const migmres_solver *s, double *out, int n
 
 // ICGS entry points on caller-provided multivectors (the OrthoManager drop-in).
 static Icgs g_icgs_default;
+static Icgs make_dgks() {
+  Icgs m;
+  m.dgks = true;
+  return m;
+}
+static Icgs g_dgks_default = make_dgks();
+extern "C" int migmres_dgks_project_normalize(migmres_mv *X, const migmres_mv *Q, double *C, int ldc,
+                                              double *B, int ldb, int *rank) {
+  return guard([&] {
+    MIG_CHECK(X && Q && C && B && rank, "dgks_project_normalize: null argument");
+    *rank = g_dgks_default.project_and_normalize(*X, *const_cast<migmres_mv *>(Q), C, ldc, B, ldb);
+  });
+}
+extern "C" int migmres_dgks_normalize(migmres_mv *X, double *B, int ldb, int *rank) {
+  return guard([&] {
+    MIG_CHECK(X && B && rank, "dgks_normalize: null argument");
+    *rank = g_dgks_default.normalize(*X, B, ldb);
+  });
+}
 extern "C" int migmres_icgs_project_normalize(migmres_mv *X, const migmres_mv *Q, double *C, int ldc,
                                               double *B, int ldb, int *rank) {
   return guard([&] {
