@@ -68,12 +68,15 @@ struct MvDesc {
 // >= n_local index the ghost block (column-major, leading dim ldg).  Row sums are
 // accumulated in stored order without contraction (Epetra GeneralMM order).
 // Row-pair SpMM (plan from make_pair_plan); vals padded by 8 entries, ghost ld even.
+// sel/nsel: optional subset of pairs (rows for launch_spmm) to compute -- the interior and
+// boundary halves of the halo overlap.
 void launch_spmm_pair(hipStream_t s, int n_local, int max_keys, const int *rowptr, const int *pptr,
                       const int *pkey, const unsigned short *pmeta, const double *vals, MvDesc X,
-                      const double *ghost, long long ldg, MvDesc Y, double alpha, double beta);
+                      const double *ghost, long long ldg, MvDesc Y, double alpha, double beta,
+                      const int *sel = nullptr, int nsel = 0);
 void launch_spmm(hipStream_t s, int row_begin, int row_end, const int *rowptr, const int *cols,
                  const double *vals, MvDesc X, int n_local, const double *ghost, long long ldg,
-                 MvDesc Y, double alpha, double beta);
+                 MvDesc Y, double alpha, double beta, const int *sel = nullptr, int nsel = 0);
 
 // Partial products for C = A^T B over `nrows` rows: writes nblocks x (L*kb) partials.
 int gemm_tn_blocks(int nrows);

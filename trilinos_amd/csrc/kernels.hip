@@ -41,10 +41,17 @@ __global__ __launch_bounds__(256) void k_spmm(int row_begin, int row_end,
                                               const double *__restrict__ vals, MvDesc X,
                                               int n_local, const double *__restrict__ ghost,
                                               long long ldg, MvDesc Y, int c0, int kc,
-                                              double alpha, double beta) {
+                                              double alpha, double beta, const int *__restrict__ sel,
+                                              int nsel) {
 #pragma clang fp contract(off)
-  const int r = row_begin + blockIdx.x * 256 + threadIdx.x;
-  if (r >= row_end) return;
+  int r = row_begin + blockIdx.x * 256 + threadIdx.x;
+  if (sel) {  // optional list of rows (interior / boundary split of the halo overlap)
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= nsel) return;
+    r = sel[t];
+  } else if (r >= row_end) {
+    return;
+  }
   const double *xc[KC];
   const double *gc[KC];
   double sum[KC];
@@ -100,23 +107,23 @@ __global__ __launch_bounds__(256) void k_spmm(int row_begin, int row_end,
 
 void launch_spmm(hipStream_t s, int row_begin, int row_end, const int *rowptr, const int *cols,
                  const double *vals, MvDesc X, int n_local, const double *ghost, long long ldg,
-                 MvDesc Y, double alpha, double beta) {
-  const int n = row_end - row_begin;
+                 MvDesc Y, double alpha, double beta, const int *sel, int nsel) {
+  const int n = sel ? nsel : row_end - row_begin;
   if (n <= 0) return;
   const int k = Y.ncols;
   const dim3 grid(cdiv(n, 256));
   for (int c0 = 0; c0 < k; c0 += 16) {
     const int kc = (k - c0) < 16 ? (k - c0) : 16;
     if (kc == 1)
-      k_spmm<1><<<grid, 256, 0, s>>>(row_begin, row_end, rowptr, cols, vals, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta);
+      k_spmm<1><<<grid, 256, 0, s>>>(row_begin, row_end, rowptr, cols, vals, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel);
     else if (kc <= 2)
-      k_spmm<2><<<grid, 256, 0, s>>>(row_begin, row_end, rowptr, cols, vals, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta);
+      k_spmm<2><<<grid, 256, 0, s>>>(row_begin, row_end, rowptr, cols, vals, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel);
     else if (kc <= 4)
-      k_spmm<4><<<grid, 256, 0, s>>>(row_begin, row_end, rowptr, cols, vals, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta);
+      k_spmm<4><<<grid, 256, 0, s>>>(row_begin, row_end, rowptr, cols, vals, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel);
     else if (kc <= 8)
-      k_spmm<8><<<grid, 256, 0, s>>>(row_begin, row_end, rowptr, cols, vals, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta);
+      k_spmm<8><<<grid, 256, 0, s>>>(row_begin, row_end, rowptr, cols, vals, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel);
     else
-      k_spmm<16><<<grid, 256, 0, s>>>(row_begin, row_end, rowptr, cols, vals, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta);
+      k_spmm<16><<<grid, 256, 0, s>>>(row_begin, row_end, rowptr, cols, vals, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel);
     LAUNCH_CHECK();
   }
 }
@@ -138,10 +145,17 @@ __global__ __launch_bounds__(256) void k_spmm_pair(int npairs, const int *__rest
                                                    const unsigned short *__restrict__ pmeta,
                                                    const double *__restrict__ vals, MvDesc X, int n_local,
                                                    const double *__restrict__ ghost, long long ldg, MvDesc Y,
-                                                   int c0, int kc, double alpha, double beta) {
+                                                   int c0, int kc, double alpha, double beta,
+                                                   const int *__restrict__ sel, int nsel) {
 #pragma clang fp contract(off)
-  const int p = blockIdx.x * 256 + threadIdx.x;
-  if (p >= npairs) return;
+  // sel: optional list of the pairs to compute (interior / boundary split of the halo overlap)
+  int p = blockIdx.x * 256 + threadIdx.x;
+  if (sel) {
+    if (p >= nsel) return;
+    p = sel[p];
+  } else if (p >= npairs) {
+    return;
+  }
   const int ra = 2 * p;
   const bool hasb = ra + 1 < n_local;
   const int ea = rowptr[ra], eb = rowptr[ra + 1], ee = hasb ? rowptr[ra + 2] : eb;
@@ -209,32 +223,36 @@ __global__ __launch_bounds__(256) void k_spmm_pair(int npairs, const int *__rest
 template <int MAXK>
 static void spmm_pair_cols(hipStream_t s, int npairs, const int *rowptr, const int *pptr, const int *pkey,
                            const unsigned short *pmeta, const double *vals, MvDesc X, int n_local,
-                           const double *ghost, long long ldg, MvDesc Y, double alpha, double beta) {
+                           const double *ghost, long long ldg, MvDesc Y, double alpha, double beta,
+                           const int *sel, int nsel) {
   const int k = Y.ncols;
-  const dim3 grid(cdiv(npairs, 256));
+  const int units = sel ? nsel : npairs;
+  if (units <= 0) return;
+  const dim3 grid(cdiv(units, 256));
   for (int c0 = 0; c0 < k; c0 += 8) {
     const int kc = (k - c0) < 8 ? (k - c0) : 8;
     if (kc == 1)
-      k_spmm_pair<1, MAXK><<<grid, 256, 0, s>>>(npairs, rowptr, pptr, pkey, pmeta, vals, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta);
+      k_spmm_pair<1, MAXK><<<grid, 256, 0, s>>>(npairs, rowptr, pptr, pkey, pmeta, vals, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel);
     else if (kc <= 2)
-      k_spmm_pair<2, MAXK><<<grid, 256, 0, s>>>(npairs, rowptr, pptr, pkey, pmeta, vals, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta);
+      k_spmm_pair<2, MAXK><<<grid, 256, 0, s>>>(npairs, rowptr, pptr, pkey, pmeta, vals, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel);
     else if (kc <= 4)
-      k_spmm_pair<4, MAXK><<<grid, 256, 0, s>>>(npairs, rowptr, pptr, pkey, pmeta, vals, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta);
+      k_spmm_pair<4, MAXK><<<grid, 256, 0, s>>>(npairs, rowptr, pptr, pkey, pmeta, vals, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel);
     else
-      k_spmm_pair<8, MAXK><<<grid, 256, 0, s>>>(npairs, rowptr, pptr, pkey, pmeta, vals, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta);
+      k_spmm_pair<8, MAXK><<<grid, 256, 0, s>>>(npairs, rowptr, pptr, pkey, pmeta, vals, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel);
     LAUNCH_CHECK();
   }
 }
 
 void launch_spmm_pair(hipStream_t s, int n_local, int max_keys, const int *rowptr, const int *pptr,
                       const int *pkey, const unsigned short *pmeta, const double *vals, MvDesc X,
-                      const double *ghost, long long ldg, MvDesc Y, double alpha, double beta) {
+                      const double *ghost, long long ldg, MvDesc Y, double alpha, double beta,
+                      const int *sel, int nsel) {
   const int npairs = (n_local + 1) / 2;
   if (npairs <= 0) return;
   if (max_keys <= 8)
-    spmm_pair_cols<8>(s, npairs, rowptr, pptr, pkey, pmeta, vals, X, n_local, ghost, ldg, Y, alpha, beta);
+    spmm_pair_cols<8>(s, npairs, rowptr, pptr, pkey, pmeta, vals, X, n_local, ghost, ldg, Y, alpha, beta, sel, nsel);
   else if (max_keys <= 12)
-    spmm_pair_cols<12>(s, npairs, rowptr, pptr, pkey, pmeta, vals, X, n_local, ghost, ldg, Y, alpha, beta);
+    spmm_pair_cols<12>(s, npairs, rowptr, pptr, pkey, pmeta, vals, X, n_local, ghost, ldg, Y, alpha, beta, sel, nsel);
   else
     throw Error(MIGMRES_EINVAL, "spmm_pair: more than 12 keys per row pair");
 }

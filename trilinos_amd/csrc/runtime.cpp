@@ -123,7 +123,8 @@ static void loop_allreduce(migmres_ctx *c, double *d, size_t n, bool max) {
   MIG_HIP(hipMemcpy(d, out.data(), sizeof(double) * n, hipMemcpyHostToDevice));
 }
 
-void migmres_ctx::p2p_begin() {
+void migmres_ctx::p2p_begin(hipStream_t s) {
+  p2p_stream = s ? s : stream;
   p2p_sends.clear();
   p2p_recvs.clear();
   if (!loop) MIG_NCCL(ncclGroupStart());
@@ -132,13 +133,13 @@ void migmres_ctx::p2p_send(const void *buf, size_t bytes, int peer) {
   if (loop)
     p2p_sends.push_back({const_cast<void *>(buf), bytes, peer});
   else
-    MIG_NCCL(ncclSend(buf, bytes, ncclChar, peer, comm, stream));
+    MIG_NCCL(ncclSend(buf, bytes, ncclChar, peer, comm, p2p_stream));
 }
 void migmres_ctx::p2p_recv(void *buf, size_t bytes, int peer) {
   if (loop)
     p2p_recvs.push_back({buf, bytes, peer});
   else
-    MIG_NCCL(ncclRecv(buf, bytes, ncclChar, peer, comm, stream));
+    MIG_NCCL(ncclRecv(buf, bytes, ncclChar, peer, comm, p2p_stream));
 }
 void migmres_ctx::p2p_end() {
   if (!loop) {
@@ -146,7 +147,7 @@ void migmres_ctx::p2p_end() {
     return;
   }
   LoopGroup &g = *loop;
-  MIG_HIP(hipStreamSynchronize(stream));
+  MIG_HIP(hipStreamSynchronize(p2p_stream));
   for (auto &m : p2p_sends) {
     std::vector<char> v(m.bytes);
     if (m.bytes) MIG_HIP(hipMemcpy(v.data(), m.buf, m.bytes, hipMemcpyDeviceToHost));
@@ -329,6 +330,9 @@ extern "C" int migmres_ctx_create(int device, int rank, int nranks, const unsign
           std::memcpy(&id, uid, 128);
           MIG_NCCL(ncclCommInitRank(&c->comm, nranks, id, rank));
         }
+        MIG_HIP(hipStreamCreateWithFlags(&c->halo_stream, hipStreamNonBlocking));
+        MIG_HIP(hipEventCreateWithFlags(&c->ev_main, hipEventDisableTiming));
+        MIG_HIP(hipEventCreateWithFlags(&c->ev_halo, hipEventDisableTiming));
       }
     } catch (...) {
       delete c;
@@ -349,6 +353,12 @@ extern "C" int migmres_ctx_destroy(migmres_ctx *c) {
     if (c->d_red) hipFree(c->d_red);
     if (c->d_coef) hipFree(c->d_coef);
     if (c->h_pinned) hipHostFree(c->h_pinned);
+    if (c->halo_stream) {
+      hipStreamSynchronize(c->halo_stream);
+      hipStreamDestroy(c->halo_stream);
+    }
+    if (c->ev_main) hipEventDestroy(c->ev_main);
+    if (c->ev_halo) hipEventDestroy(c->ev_halo);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
   });
@@ -637,8 +647,9 @@ void mv_assign(const migmres_mv &A, migmres_mv &Y) {
 // distributed CRS operator
 // ------------------------------------------------------------------------------------
 migmres_crs::~migmres_crs() {
-  for (void *p : {(void *)d_rowptr, (void *)d_cols, (void *)d_export, (void *)d_vals,
-                  (void *)d_send, (void *)d_ghost, (void *)d_pptr, (void *)d_pkey, (void *)d_pmeta})
+  for (void *p : {(void *)d_rowptr, (void *)d_cols, (void *)d_export, (void *)d_vals, (void *)d_send,
+                  (void *)d_ghost, (void *)d_pptr, (void *)d_pkey, (void *)d_pmeta, (void *)d_sel_int,
+                  (void *)d_sel_bnd})
     if (p) hipFree(p);
 }
 
@@ -706,7 +717,7 @@ migmres_crs *crs_create(migmres_ctx *ctx, long long n_global, long long first, i
       MIG_HIP(hipMalloc(&d_give, sizeof(long long) * (total_give > 0 ? total_give : 1)));
       if (n_remote)
         MIG_HIP(hipMemcpy(d_req, p.remote_gids.data(), sizeof(long long) * n_remote, hipMemcpyHostToDevice));
-      ctx->p2p_begin();
+      ctx->p2p_begin(ctx->stream);
       for (auto &nb : A->recv_nbrs) ctx->p2p_send(d_req + nb.offset, sizeof(long long) * nb.count, nb.pid);
       for (int q = 0; q < P; ++q)
         if (give_cnt[(size_t)q] > 0)
@@ -756,6 +767,31 @@ migmres_crs *crs_create(migmres_ctx *ctx, long long n_global, long long first, i
         A->pair_max_keys = pp.max_keys;
       }
     }
+    if (n_remote > 0) {
+      // interior / boundary units for the halo overlap (a unit is a row pair with the
+      // row-pair kernel, else a row; boundary = reads at least one ghost column)
+      const int unit = A->use_pairs ? 2 : 1;
+      const int nunits = (n_local + unit - 1) / unit;
+      std::vector<int> sel_int, sel_bnd;
+      for (int u = 0; u < nunits; ++u) {
+        bool ghost = false;
+        for (int r = u * unit; r < std::min(n_local, (u + 1) * unit) && !ghost; ++r)
+          for (long long e = rowptr[r]; e < rowptr[r + 1]; ++e)
+            if (lcols[(size_t)e] >= n_local) {
+              ghost = true;
+              break;
+            }
+        (ghost ? sel_bnd : sel_int).push_back(u);
+      }
+      A->n_sel_int = (int)sel_int.size();
+      A->n_sel_bnd = (int)sel_bnd.size();
+      MIG_HIP(hipMalloc(&A->d_sel_int, sizeof(int) * (sel_int.size() + 1)));
+      MIG_HIP(hipMalloc(&A->d_sel_bnd, sizeof(int) * (sel_bnd.size() + 1)));
+      if (!sel_int.empty())
+        MIG_HIP(hipMemcpy(A->d_sel_int, sel_int.data(), sizeof(int) * sel_int.size(), hipMemcpyHostToDevice));
+      if (!sel_bnd.empty())
+        MIG_HIP(hipMemcpy(A->d_sel_bnd, sel_bnd.data(), sizeof(int) * sel_bnd.size(), hipMemcpyHostToDevice));
+    }
     if (!A->export_lids.empty()) {
       MIG_HIP(hipMalloc(&A->d_export, sizeof(int) * A->export_lids.size()));
       MIG_HIP(hipMemcpy(A->d_export, A->export_lids.data(), sizeof(int) * A->export_lids.size(),
@@ -775,8 +811,19 @@ void crs_apply(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, double alpha,
   const int k = X.ncols;
   const int n_remote = (int)A.plan.remote_lids.size();
   const int n_export = (int)A.export_lids.size();
-  if (c->nranks > 1 && (n_remote > 0 || n_export > 0)) {
+  const bool halo = c->nranks > 1 && (n_remote > 0 || n_export > 0);
+  auto spmm = [&](const int *sel, int nsel) {
+    if (A.use_pairs)
+      launch_spmm_pair(c->stream, A.n_local, A.pair_max_keys, A.d_rowptr, A.d_pptr, A.d_pkey, A.d_pmeta, A.d_vals,
+                       X.desc(), A.d_ghost, A.ldg, Y.desc(), alpha, beta, sel, nsel);
+    else
+      launch_spmm(c->stream, 0, A.n_local, A.d_rowptr, A.d_cols, A.d_vals, X.desc(), A.n_local, A.d_ghost, A.ldg,
+                  Y.desc(), alpha, beta, sel, nsel);
+  };
+  if (halo) {
     if (k > A.halo_k) {
+      MIG_HIP(hipStreamSynchronize(c->stream));
+      MIG_HIP(hipStreamSynchronize(c->halo_stream));
       if (A.d_send) hipFree(A.d_send);
       if (A.d_ghost) hipFree(A.d_ghost);
       A.d_send = A.d_ghost = nullptr;
@@ -786,9 +833,14 @@ void crs_apply(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, double alpha,
       MIG_HIP(hipMemset(A.d_ghost, 0, sizeof(double) * ((size_t)A.ldg * k + 2)));
       A.halo_k = k;
     }
+    // Import on the halo stream (Epetra_Import through Epetra_MpiDistributor::Do), ordered
+    // after everything already queued on the context stream (X is ready, the previous
+    // apply's boundary rows have read the ghost block).
     auto t0 = std::chrono::steady_clock::now();
-    launch_pack(c->stream, X.desc(), A.d_export, n_export, A.d_send, k);
-    c->p2p_begin();
+    MIG_HIP(hipEventRecord(c->ev_main, c->stream));
+    MIG_HIP(hipStreamWaitEvent(c->halo_stream, c->ev_main, 0));
+    launch_pack(c->halo_stream, X.desc(), A.d_export, n_export, A.d_send, k);
+    c->p2p_begin(c->halo_stream);
     for (auto &nb : A.send_nbrs)
       for (int col = 0; col < k; ++col)
         c->p2p_send(A.d_send + (size_t)col * n_export + nb.offset, sizeof(double) * nb.count, nb.pid);
@@ -796,15 +848,19 @@ void crs_apply(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, double alpha,
       for (int col = 0; col < k; ++col)
         c->p2p_recv(A.d_ghost + (size_t)col * A.ldg + nb.offset, sizeof(double) * nb.count, nb.pid);
     c->p2p_end();
+    MIG_HIP(hipEventRecord(c->ev_halo, c->halo_stream));
     c->comm_seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
   ProfScope ps(c, K_SPMM, 12.0 * A.nnz + 4.0 * (A.n_local + 1) + 8.0 * A.n_local * k * (beta == 0.0 ? 2.0 : 3.0));
-  if (A.use_pairs)
-    launch_spmm_pair(c->stream, A.n_local, A.pair_max_keys, A.d_rowptr, A.d_pptr, A.d_pkey, A.d_pmeta, A.d_vals, X.desc(),
-                     A.d_ghost, A.ldg, Y.desc(), alpha, beta);
-  else
-    launch_spmm(c->stream, 0, A.n_local, A.d_rowptr, A.d_cols, A.d_vals, X.desc(), A.n_local, A.d_ghost,
-                A.ldg, Y.desc(), alpha, beta);
+  if (halo && A.d_sel_int) {
+    // interior rows while the halo is in flight, then the rows that read ghost columns
+    spmm(A.d_sel_int, A.n_sel_int);
+    MIG_HIP(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
+    spmm(A.d_sel_bnd, A.n_sel_bnd);
+  } else {
+    if (halo) MIG_HIP(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
+    spmm(nullptr, 0);
+  }
 }
 
 }  // namespace migmres

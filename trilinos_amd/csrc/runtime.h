@@ -53,6 +53,11 @@ struct migmres_ctx {
   void dev_free(void *p, size_t rounded);
   void pool_trim();
   hipStream_t stream = nullptr;
+  // second stream for the halo exchange (nranks > 1): pack + RCCL point-to-point run there
+  // while the interior rows' SpMM runs on `stream` (events order the two)
+  hipStream_t halo_stream = nullptr;
+  hipEvent_t ev_main = nullptr, ev_halo = nullptr;
+  hipStream_t p2p_stream = nullptr;  // stream of the open p2p group
   ncclComm_t comm = nullptr;
   // In-process multi-rank emulation for tests (all ranks' contexts in one process on one
   // device, one host thread per rank; selected by a "MIGLOOP1" unique id): collectives and
@@ -65,7 +70,7 @@ struct migmres_ctx {
   };
   std::vector<P2p> p2p_sends, p2p_recvs;
   // grouped point-to-point exchange (ncclGroupStart/Send/Recv/GroupEnd on the stream)
-  void p2p_begin();
+  void p2p_begin(hipStream_t s = nullptr);  // default: the context stream
   void p2p_send(const void *buf, size_t bytes, int peer);
   void p2p_recv(void *buf, size_t bytes, int peer);
   void p2p_end();
@@ -126,6 +131,10 @@ struct migmres_crs {
   unsigned short *d_pmeta = nullptr;
   bool use_pairs = false;
   int pair_max_keys = 0;
+  // interior / boundary split (units = pairs with the row-pair kernel, else rows): interior
+  // units read no ghost column and run while the halo exchange is in flight
+  int *d_sel_int = nullptr, *d_sel_bnd = nullptr;
+  int n_sel_int = 0, n_sel_bnd = 0;
   double *d_send = nullptr, *d_ghost = nullptr;
   long long ldg = 0;  // ghost block leading dimension: n_remote rounded up to even, padding zero
   int halo_k = 0;
