@@ -249,12 +249,26 @@ void launch_spmm_pair(hipStream_t s, int n_local, int max_keys, const int *rowpt
                       const int *sel, int nsel) {
   const int npairs = (n_local + 1) / 2;
   if (npairs <= 0) return;
-  if (max_keys <= 8)
-    spmm_pair_cols<8>(s, npairs, rowptr, pptr, pkey, pmeta, vals, X, n_local, ghost, ldg, Y, alpha, beta, sel, nsel);
-  else if (max_keys <= 12)
-    spmm_pair_cols<12>(s, npairs, rowptr, pptr, pkey, pmeta, vals, X, n_local, ghost, ldg, Y, alpha, beta, sel, nsel);
-  else
-    throw Error(MIGMRES_EINVAL, "spmm_pair: more than 12 keys per row pair");
+  // instantiated for the exact key count (a key slot past every pair's count would still
+  // issue its load: 8 loads per column instead of 7 on a 7-point stencil)
+#define PAIR_CASE(K) \
+  case K:            \
+    spmm_pair_cols<K>(s, npairs, rowptr, pptr, pkey, pmeta, vals, X, n_local, ghost, ldg, Y, alpha, beta, sel, nsel); \
+    break;
+  switch (max_keys < 4 ? 4 : max_keys) {
+    PAIR_CASE(4)
+    PAIR_CASE(5)
+    PAIR_CASE(6)
+    PAIR_CASE(7)
+    PAIR_CASE(8)
+    PAIR_CASE(9)
+    PAIR_CASE(10)
+    PAIR_CASE(11)
+    PAIR_CASE(12)
+    default:
+      throw Error(MIGMRES_EINVAL, "spmm_pair: more than 12 keys per row pair");
+  }
+#undef PAIR_CASE
 }
 
 // -------------------------------------------------------------------------------------
