@@ -70,10 +70,9 @@ struct MvDesc {
 // Row-pair SpMM (plan from make_pair_plan); vals padded by 8 entries, ghost ld even.
 // sel/nsel: optional subset of pairs (rows for launch_spmm) to compute -- the interior and
 // boundary halves of the halo overlap.
-void launch_spmm_pair(hipStream_t s, int n_local, int max_keys, const int *rowptr, const int *pptr,
-                      const int *pkey, const unsigned short *pmeta, const double *vals, MvDesc X,
-                      const double *ghost, long long ldg, MvDesc Y, double alpha, double beta,
-                      const int *sel = nullptr, int nsel = 0);
+void launch_spmm_pair(hipStream_t s, int n_local, int max_keys, int rmax, const double *sv, const int *sk,
+                      const unsigned short *sm, MvDesc X, const double *ghost, long long ldg, MvDesc Y,
+                      double alpha, double beta, const int *sel = nullptr, int nsel = 0);
 void launch_spmm(hipStream_t s, int row_begin, int row_end, const int *rowptr, const int *cols,
                  const double *vals, MvDesc X, int n_local, const double *ghost, long long ldg,
                  MvDesc Y, double alpha, double beta, const int *sel = nullptr, int nsel = 0);

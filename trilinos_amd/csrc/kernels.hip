@@ -140,10 +140,9 @@ void launch_spmm(hipStream_t s, int row_begin, int row_end, const int *rowptr, c
 constexpr int PAIR_MAXR = 8;
 
 template <int KC, int PAIR_MAXK>
-__global__ __launch_bounds__(256) void k_spmm_pair(int npairs, const int *__restrict__ rowptr,
-                                                   const int *__restrict__ pptr, const int *__restrict__ pkey,
-                                                   const unsigned short *__restrict__ pmeta,
-                                                   const double *__restrict__ vals, MvDesc X, int n_local,
+__global__ __launch_bounds__(256) void k_spmm_pair(int npairs, int rmax, const double *__restrict__ sv,
+                                                   const int *__restrict__ sk,
+                                                   const unsigned short *__restrict__ sm, MvDesc X, int n_local,
                                                    const double *__restrict__ ghost, long long ldg, MvDesc Y,
                                                    int c0, int kc, double alpha, double beta,
                                                    const int *__restrict__ sel, int nsel) {
@@ -158,23 +157,26 @@ __global__ __launch_bounds__(256) void k_spmm_pair(int npairs, const int *__rest
   }
   const int ra = 2 * p;
   const bool hasb = ra + 1 < n_local;
-  const int ea = rowptr[ra], eb = rowptr[ra + 1], ee = hasb ? rowptr[ra + 2] : eb;
+  // SELL-64 plan (make_pair_sell): slot j of the 64 pairs of a wave is contiguous
+  const long long chunk = p >> 6;
+  const int lane = p & 63;
+  const double *va_p = sv + chunk * 2 * rmax * 64 + lane;
+  const double *vb_p = va_p + (long long)rmax * 64;
   double va[PAIR_MAXR], vb[PAIR_MAXR];
 #pragma unroll
-  for (int j = 0; j < PAIR_MAXR; ++j) {  // vals is padded by PAIR_MAXR entries
-    va[j] = vals[ea + j];
-    vb[j] = vals[eb + j];
+  for (int j = 0; j < PAIR_MAXR; ++j) {
+    va[j] = j < rmax ? va_p[j * 64] : 0.0;
+    vb[j] = j < rmax ? vb_p[j * 64] : 0.0;
   }
-  (void)ee;
-  const int u0 = pptr[p], nu = pptr[p + 1] - u0;
+  const int *kp = sk + chunk * PAIR_MAXK * 64 + lane;
+  const unsigned short *mp = sm + chunk * PAIR_MAXK * 64 + lane;
   int key[PAIR_MAXK];
   double cx[PAIR_MAXK][4];  // coefficient taking (row a low, row a high, row b low, row b high)
   unsigned long long use = 0;  // bit 4u + s: slot s of key u is used
 #pragma unroll
   for (int u = 0; u < PAIR_MAXK; ++u) {
-    const int uu = u < nu ? u0 + u : u0 + (nu > 0 ? nu - 1 : 0);
-    key[u] = pkey[uu];
-    const unsigned m = u < nu ? pmeta[uu] : 0xFFFFu;
+    key[u] = kp[u * 64];
+    const unsigned m = mp[u * 64];
 #pragma unroll
     for (int sl = 0; sl < 4; ++sl) {
       const int idx = (m >> (4 * sl)) & 0xF;
@@ -221,10 +223,9 @@ __global__ __launch_bounds__(256) void k_spmm_pair(int npairs, const int *__rest
 }
 
 template <int MAXK>
-static void spmm_pair_cols(hipStream_t s, int npairs, const int *rowptr, const int *pptr, const int *pkey,
-                           const unsigned short *pmeta, const double *vals, MvDesc X, int n_local,
-                           const double *ghost, long long ldg, MvDesc Y, double alpha, double beta,
-                           const int *sel, int nsel) {
+static void spmm_pair_cols(hipStream_t s, int npairs, int rmax, const double *sv, const int *sk,
+                           const unsigned short *sm, MvDesc X, int n_local, const double *ghost, long long ldg,
+                           MvDesc Y, double alpha, double beta, const int *sel, int nsel) {
   const int k = Y.ncols;
   const int units = sel ? nsel : npairs;
   if (units <= 0) return;
@@ -232,30 +233,32 @@ static void spmm_pair_cols(hipStream_t s, int npairs, const int *rowptr, const i
   for (int c0 = 0; c0 < k; c0 += 8) {
     const int kc = (k - c0) < 8 ? (k - c0) : 8;
     if (kc == 1)
-      k_spmm_pair<1, MAXK><<<grid, 256, 0, s>>>(npairs, rowptr, pptr, pkey, pmeta, vals, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel);
+      k_spmm_pair<1, MAXK><<<grid, 256, 0, s>>>(npairs, rmax, sv, sk, sm, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel);
     else if (kc <= 2)
-      k_spmm_pair<2, MAXK><<<grid, 256, 0, s>>>(npairs, rowptr, pptr, pkey, pmeta, vals, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel);
+      k_spmm_pair<2, MAXK><<<grid, 256, 0, s>>>(npairs, rmax, sv, sk, sm, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel);
     else if (kc <= 4)
-      k_spmm_pair<4, MAXK><<<grid, 256, 0, s>>>(npairs, rowptr, pptr, pkey, pmeta, vals, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel);
+      k_spmm_pair<4, MAXK><<<grid, 256, 0, s>>>(npairs, rmax, sv, sk, sm, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel);
     else
-      k_spmm_pair<8, MAXK><<<grid, 256, 0, s>>>(npairs, rowptr, pptr, pkey, pmeta, vals, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel);
+      k_spmm_pair<8, MAXK><<<grid, 256, 0, s>>>(npairs, rmax, sv, sk, sm, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel);
     LAUNCH_CHECK();
   }
 }
 
-void launch_spmm_pair(hipStream_t s, int n_local, int max_keys, const int *rowptr, const int *pptr,
-                      const int *pkey, const unsigned short *pmeta, const double *vals, MvDesc X,
-                      const double *ghost, long long ldg, MvDesc Y, double alpha, double beta,
-                      const int *sel, int nsel) {
+void launch_spmm_pair(hipStream_t s, int n_local, int max_keys, int rmax, const double *sv, const int *sk,
+                      const unsigned short *sm, MvDesc X, const double *ghost, long long ldg, MvDesc Y,
+                      double alpha, double beta, const int *sel, int nsel) {
   const int npairs = (n_local + 1) / 2;
   if (npairs <= 0) return;
-  // instantiated for the exact key count (a key slot past every pair's count would still
-  // issue its load: 8 loads per column instead of 7 on a 7-point stencil)
+  if (rmax > PAIR_MAXR) throw Error(MIGMRES_EINVAL, "spmm_pair: rows longer than 8 entries");
+  // instantiated for the exact key count (the SELL plan is laid out with that stride)
 #define PAIR_CASE(K) \
   case K:            \
-    spmm_pair_cols<K>(s, npairs, rowptr, pptr, pkey, pmeta, vals, X, n_local, ghost, ldg, Y, alpha, beta, sel, nsel); \
+    spmm_pair_cols<K>(s, npairs, rmax, sv, sk, sm, X, n_local, ghost, ldg, Y, alpha, beta, sel, nsel); \
     break;
-  switch (max_keys < 4 ? 4 : max_keys) {
+  switch (max_keys) {
+    PAIR_CASE(1)
+    PAIR_CASE(2)
+    PAIR_CASE(3)
     PAIR_CASE(4)
     PAIR_CASE(5)
     PAIR_CASE(6)

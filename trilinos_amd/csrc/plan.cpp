@@ -242,4 +242,36 @@ bool make_pair_plan(int n_local, const long long *rowptr, const int *xcols, Pair
   return true;
 }
 
+void make_pair_sell(int n_local, const long long *rowptr, const double *lvals, const PairPlan &plan, PairSell &out) {
+  const int P = (n_local + 1) / 2;
+  const int nchunks = (P + 63) / 64;
+  int rmax = 1;
+  for (int r = 0; r < n_local; ++r) rmax = std::max(rmax, (int)(rowptr[r + 1] - rowptr[r]));
+  const int maxk = std::max(plan.max_keys, 1);
+  out.rmax = rmax;
+  out.maxk = maxk;
+  out.v.assign((size_t)nchunks * 2 * rmax * 64, 0.0);
+  out.k.assign((size_t)nchunks * maxk * 64, 0);
+  out.m.assign((size_t)nchunks * maxk * 64, 0xFFFF);
+  for (int p = 0; p < P; ++p) {
+    const int chunk = p / 64, lane = p % 64;
+    for (int h = 0; h < 2; ++h) {
+      const int r = 2 * p + h;
+      if (r >= n_local) continue;
+      for (long long e = rowptr[r]; e < rowptr[r + 1]; ++e)
+        out.v[(((size_t)chunk * 2 + h) * rmax + (size_t)(e - rowptr[r])) * 64 + lane] = lvals[e];
+    }
+    const int u0 = plan.ptr[(size_t)p], nu = plan.ptr[(size_t)p + 1] - u0;
+    for (int u = 0; u < maxk; ++u) {
+      const size_t at = ((size_t)chunk * maxk + u) * 64 + lane;
+      if (u < nu) {
+        out.k[at] = plan.key[(size_t)(u0 + u)];
+        out.m[at] = plan.meta[(size_t)(u0 + u)];
+      } else {
+        out.k[at] = nu > 0 ? plan.key[(size_t)(u0 + nu - 1)] : p;  // a valid address, map empty
+      }
+    }
+  }
+}
+
 }  // namespace migmres

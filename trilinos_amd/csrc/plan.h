@@ -45,6 +45,19 @@ struct PairPlan {
 };
 bool make_pair_plan(int n_local, const long long *rowptr, const int *xcols, PairPlan &out);
 
+// The pair plan in the layout k_spmm_pair reads ("SELL-64": per wave of 64 row pairs, slot s
+// of all 64 pairs is contiguous), so that every lane's coefficient / key loads coalesce:
+//   v[((chunk * 2 + h) * rmax + j) * 64 + lane]  entry j of row 2p + h (0 past the row's end)
+//   k[(chunk * maxk + u) * 64 + lane], m[...]    key u and its half map (unused: last key, 0xFFFF)
+// with p = 64 chunk + lane, rmax = longest row, maxk = plan.max_keys.
+struct PairSell {
+  std::vector<double> v;
+  std::vector<int> k;
+  std::vector<unsigned short> m;
+  int rmax = 0, maxk = 0;
+};
+void make_pair_sell(int n_local, const long long *rowptr, const double *lvals, const PairPlan &plan, PairSell &out);
+
 void galeri_rows(const std::string &kind, int nx, int ny, int nz, long long first, int n_local,
                  std::vector<long long> &rowptr, std::vector<long long> &gcols,
                  std::vector<double> &vals);

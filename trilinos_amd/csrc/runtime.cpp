@@ -648,7 +648,7 @@ void mv_assign(const migmres_mv &A, migmres_mv &Y) {
 // ------------------------------------------------------------------------------------
 migmres_crs::~migmres_crs() {
   for (void *p : {(void *)d_rowptr, (void *)d_cols, (void *)d_export, (void *)d_vals, (void *)d_send,
-                  (void *)d_ghost, (void *)d_pptr, (void *)d_pkey, (void *)d_pmeta, (void *)d_sel_int,
+                  (void *)d_ghost, (void *)d_psv, (void *)d_psk, (void *)d_psm, (void *)d_sel_int,
                   (void *)d_sel_bnd})
     if (p) hipFree(p);
 }
@@ -755,16 +755,18 @@ migmres_crs *crs_create(migmres_ctx *ctx, long long n_global, long long first, i
     {
       PairPlan pp;
       const char *np = std::getenv("MIGMRES_NO_PAIR_SPMM");
-      if (!(np && np[0] == '1') && make_pair_plan(n_local, rowptr, lcols.data(), pp)) {
-        MIG_HIP(hipMalloc(&A->d_pptr, sizeof(int) * pp.ptr.size()));
-        MIG_HIP(hipMalloc(&A->d_pkey, sizeof(int) * pp.key.size()));
-        MIG_HIP(hipMalloc(&A->d_pmeta, sizeof(unsigned short) * pp.meta.size()));
-        MIG_HIP(hipMemcpy(A->d_pptr, pp.ptr.data(), sizeof(int) * pp.ptr.size(), hipMemcpyHostToDevice));
-        MIG_HIP(hipMemcpy(A->d_pkey, pp.key.data(), sizeof(int) * pp.key.size(), hipMemcpyHostToDevice));
-        MIG_HIP(hipMemcpy(A->d_pmeta, pp.meta.data(), sizeof(unsigned short) * pp.meta.size(),
-                          hipMemcpyHostToDevice));
+      if (!(np && np[0] == '1') && n_local > 0 && make_pair_plan(n_local, rowptr, lcols.data(), pp)) {
+        PairSell ps;
+        make_pair_sell(n_local, rowptr, lvals.data(), pp, ps);
+        MIG_HIP(hipMalloc(&A->d_psv, sizeof(double) * ps.v.size()));
+        MIG_HIP(hipMalloc(&A->d_psk, sizeof(int) * ps.k.size()));
+        MIG_HIP(hipMalloc(&A->d_psm, sizeof(unsigned short) * ps.m.size()));
+        MIG_HIP(hipMemcpy(A->d_psv, ps.v.data(), sizeof(double) * ps.v.size(), hipMemcpyHostToDevice));
+        MIG_HIP(hipMemcpy(A->d_psk, ps.k.data(), sizeof(int) * ps.k.size(), hipMemcpyHostToDevice));
+        MIG_HIP(hipMemcpy(A->d_psm, ps.m.data(), sizeof(unsigned short) * ps.m.size(), hipMemcpyHostToDevice));
         A->use_pairs = true;
-        A->pair_max_keys = pp.max_keys;
+        A->pair_max_keys = ps.maxk;
+        A->pair_rmax = ps.rmax;
       }
     }
     if (n_remote > 0) {
@@ -814,8 +816,8 @@ void crs_apply(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, double alpha,
   const bool halo = c->nranks > 1 && (n_remote > 0 || n_export > 0);
   auto spmm = [&](const int *sel, int nsel) {
     if (A.use_pairs)
-      launch_spmm_pair(c->stream, A.n_local, A.pair_max_keys, A.d_rowptr, A.d_pptr, A.d_pkey, A.d_pmeta, A.d_vals,
-                       X.desc(), A.d_ghost, A.ldg, Y.desc(), alpha, beta, sel, nsel);
+      launch_spmm_pair(c->stream, A.n_local, A.pair_max_keys, A.pair_rmax, A.d_psv, A.d_psk, A.d_psm, X.desc(),
+                       A.d_ghost, A.ldg, Y.desc(), alpha, beta, sel, nsel);
     else
       launch_spmm(c->stream, 0, A.n_local, A.d_rowptr, A.d_cols, A.d_vals, X.desc(), A.n_local, A.d_ghost, A.ldg,
                   Y.desc(), alpha, beta, sel, nsel);

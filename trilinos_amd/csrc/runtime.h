@@ -127,10 +127,11 @@ struct migmres_crs {
   int *d_rowptr = nullptr, *d_cols = nullptr, *d_export = nullptr;
   double *d_vals = nullptr;  // padded by 8 zero entries (row-pair kernel reads 8 per row)
   // row-pair gather plan (k_spmm_pair); null when the matrix does not fit it
-  int *d_pptr = nullptr, *d_pkey = nullptr;
-  unsigned short *d_pmeta = nullptr;
+  double *d_psv = nullptr;  // SELL-64 layout of the pair plan (make_pair_sell)
+  int *d_psk = nullptr;
+  unsigned short *d_psm = nullptr;
   bool use_pairs = false;
-  int pair_max_keys = 0;
+  int pair_max_keys = 0, pair_rmax = 0;
   // interior / boundary split (units = pairs with the row-pair kernel, else rows): interior
   // units read no ghost column and run while the halo exchange is in flight
   int *d_sel_int = nullptr, *d_sel_bnd = nullptr;
