@@ -162,12 +162,18 @@ __global__ __launch_bounds__(256) void k_spmm_pair(int npairs, int rmax, const d
   const int lane = p & 63;
   const double *va_p = sv + chunk * 2 * rmax * 64 + lane;
   const double *vb_p = va_p + (long long)rmax * 64;
-  double va[PAIR_MAXR], vb[PAIR_MAXR];
+  // the pair's coefficients go through a per-thread LDS slot so that each (key, half, row)
+  // picks its entry with one indexed read instead of an 8-way select chain
+  __shared__ double vlds[256][2 * PAIR_MAXR + 1];
+  double *myv = vlds[threadIdx.x];
 #pragma unroll
   for (int j = 0; j < PAIR_MAXR; ++j) {
-    va[j] = j < rmax ? va_p[j * 64] : 0.0;
-    vb[j] = j < rmax ? vb_p[j * 64] : 0.0;
+    if (j < rmax) {
+      myv[j] = va_p[j * 64];
+      myv[PAIR_MAXR + j] = vb_p[j * 64];
+    }
   }
+  myv[2 * PAIR_MAXR] = 0.0;
   const int *kp = sk + chunk * PAIR_MAXK * 64 + lane;
   const unsigned short *mp = sm + chunk * PAIR_MAXK * 64 + lane;
   int key[PAIR_MAXK];
@@ -180,11 +186,9 @@ __global__ __launch_bounds__(256) void k_spmm_pair(int npairs, int rmax, const d
 #pragma unroll
     for (int sl = 0; sl < 4; ++sl) {
       const int idx = (m >> (4 * sl)) & 0xF;
-      double v = 0.0;
-#pragma unroll
-      for (int j = 0; j < PAIR_MAXR; ++j) v = (idx == j) ? (sl < 2 ? va[j] : vb[j]) : v;
-      cx[u][sl] = v;
-      use |= (idx != 0xF ? 1ull : 0ull) << (4 * u + sl);
+      const bool used = idx != 0xF;
+      cx[u][sl] = myv[used ? (sl < 2 ? 0 : PAIR_MAXR) + idx : 2 * PAIR_MAXR];
+      use |= (used ? 1ull : 0ull) << (4 * u + sl);
     }
   }
 #pragma unroll
