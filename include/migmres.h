@@ -42,6 +42,7 @@ typedef struct migmres_ctx migmres_ctx;
 typedef struct migmres_crs migmres_crs;
 typedef struct migmres_mv migmres_mv;
 typedef struct migmres_solver migmres_solver;
+typedef struct migmres_prec migmres_prec;
 
 /* error codes */
 #define MIGMRES_OK 0
@@ -117,10 +118,15 @@ int migmres_plan_pairs(int n_local, const long long *rowptr, const int *xcols, i
 int migmres_crs_create(migmres_ctx *ctx, long long n_global, long long first, int n_local,
                        const long long *rowptr, const long long *gcols, const double *vals,
                        migmres_crs **out);
-/* Galeri generators built natively on the host of each rank ("Laplace2D",
- * "Laplace3D"); nz ignored for 2-D. */
+/* Galeri generators built natively on the host of each rank ("Laplace2D", "Laplace3D",
+ * "Brick3D" = the 27-point Xpetra Brick3D with a = 26, b..g = -1); nz ignored for 2-D. */
 int migmres_crs_create_galeri(migmres_ctx *ctx, const char *kind, int nx, int ny, int nz,
                               migmres_crs **out);
+/* The same generator on the host only: rows [first, first+n_local) with GLOBAL columns in
+ * insertion order.  *nnz_out always set; the arrays are filled when non-NULL (rowptr_out
+ * n_local+1 entries, gcols_out / vals_out *nnz_out entries). */
+int migmres_plan_galeri(const char *kind, int nx, int ny, int nz, long long first, int n_local,
+                        long long *rowptr_out, long long *gcols_out, double *vals_out, long long *nnz_out);
 int migmres_crs_destroy(migmres_crs *A);
 int migmres_crs_info(const migmres_crs *A, long long *n_global, long long *first, int *n_local,
                      int *n_cols, long long *nnz_local, int *n_remote, int *n_export);
@@ -177,16 +183,37 @@ int migmres_dgks_project_normalize(migmres_mv *X, const migmres_mv *Q, double *C
                                    double *B, int ldb, int *rank);
 int migmres_dgks_normalize(migmres_mv *X, double *B, int ldb, int *rank);
 
+/* ---------------- preconditioner (Ifpack2::Relaxation "Jacobi") ---------------- */
+
+/* Point Jacobi on A's local rows: Ifpack2::Relaxation with "relaxation: type" = "Jacobi",
+ * "relaxation: sweeps" = sweeps, "relaxation: damping factor" = damping, zero starting
+ * solution (ifpack2/src/Ifpack2_Relaxation_def.hpp:1390-1454 ApplyInverseJacobi; the
+ * inverse diagonal as compute() :1240-1270).  A must outlive the preconditioner. */
+int migmres_jacobi_create(migmres_crs *A, int sweeps, double damping, migmres_prec **out);
+int migmres_prec_destroy(migmres_prec *M);
+/* Y = M X (Ifpack2::Relaxation::apply, alpha = 1, beta = 0); X and Y must not alias. */
+int migmres_prec_apply(migmres_prec *M, const migmres_mv *X, migmres_mv *Y);
+/* The stored inverse diagonal (n_local doubles). */
+int migmres_prec_diagonal(const migmres_prec *M, double *dinv_out);
+
 /* ---------------- solver manager (Belos::BlockGmresSolMgr) ---------------- */
 
 int migmres_solver_create(migmres_ctx *ctx, migmres_solver **out);
 int migmres_solver_destroy(migmres_solver *s);
-/* Belos ParameterList names: "Block Size", "Num Blocks", "Maximum Iterations",
- * "Maximum Restarts", "Convergence Tolerance", "Adaptive Block Size",
- * "Orthogonalization" ("ICGS"), "Verbosity", "Output Frequency". */
+/* Belos ParameterList names (BelosBlockGmresSolMgr.hpp:438-486): "Block Size", "Num Blocks",
+ * "Maximum Iterations", "Maximum Restarts", "Convergence Tolerance", "Adaptive Block Size",
+ * "Flexible Gmres", "Explicit Residual Test", "Orthogonalization" ("ICGS" | "DGKS"),
+ * "Implicit Residual Scaling", "Explicit Residual Scaling" ("Norm of Initial Residual" |
+ * "Norm of Preconditioned Initial Residual" | "Norm of RHS" | "None"), "Verbosity",
+ * "Output Frequency". */
 int migmres_solver_set_int(migmres_solver *s, const char *name, long long value);
 int migmres_solver_set_double(migmres_solver *s, const char *name, double value);
 int migmres_solver_set_string(migmres_solver *s, const char *name, const char *value);
+/* LinearProblem::setLeftPrec / setRightPrec (BelosLinearProblem.hpp:170-175): side
+ * MIGMRES_LEFT_PREC or MIGMRES_RIGHT_PREC; M == NULL removes it.  The solver borrows M. */
+#define MIGMRES_LEFT_PREC 0
+#define MIGMRES_RIGHT_PREC 1
+int migmres_solver_set_prec(migmres_solver *s, int side, migmres_prec *M);
 /* LinearProblem(A, X, B).setProblem() + solve(); X is updated in place.
  * *converged = 1 for Belos::Converged, 0 for Unconverged. */
 int migmres_solver_solve(migmres_solver *s, migmres_crs *A, migmres_mv *X, const migmres_mv *B,
@@ -198,7 +225,7 @@ int migmres_solver_loa_detected(const migmres_solver *s, int *loa);
  * Returns the number of rows via *nrows; pass out == NULL to query. */
 int migmres_solver_history(const migmres_solver *s, double *out, int *nrows, int *ncols);
 /* Counters: [0] operator applies, [1] explicit residual checks, [2] restarts,
- * [3] blkOrthoSing fallbacks, [4] block iterations. */
+ * [3] blkOrthoSing fallbacks, [4] block iterations, [5] preconditioner applies. */
 int migmres_solver_counters(const migmres_solver *s, long long *out, int n);
 /* Seconds spent in named phases: [0] total solve, [1] SpMM, [2] orthogonalization,
  * [3] host least-squares, [4] communication, [5] status tests, [6] restarts, [7] setup.

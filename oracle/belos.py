@@ -210,26 +210,52 @@ LP_AUGMENT_SEED = 20250219  # MvRandom stream for augmented right-hand sides
 
 
 class LinearProblem:
-    """BelosLinearProblem for an unpreconditioned operator (BelosLinearProblem.hpp)."""
+    """BelosLinearProblem (BelosLinearProblem.hpp) with optional left/right preconditioners
+    (callables Y = M(X), e.g. oracle.ifpack2.Jacobi)."""
 
-    def __init__(self, A, X, B):
+    def __init__(self, A, X, B, left=None, right=None):
         self.A = A          # callable: Y = A(X)
+        self.LP, self.RP = left, right
         self.X = np.array(X, dtype=np.float64, copy=True)
         self.B = np.array(B, dtype=np.float64, copy=True)
         self.n_apply = 0
+        self.n_prec = 0
         self.ls_num = 0
         self.ls_idx = []
         self.aug_seed = LP_AUGMENT_SEED
 
-    def apply(self, x):
+    def _op(self, x):
         self.n_apply += 1
         return self.A(x)
 
+    def _prec(self, M, x):
+        self.n_prec += 1
+        return M(x)
+
+    def apply(self, x):
+        """apply (BelosLinearProblem.hpp:989-1072): y = M_L A M_R x."""
+        if self.RP is not None:
+            x = self._prec(self.RP, x)
+        y = self._op(x)
+        if self.LP is not None:
+            y = self._prec(self.LP, y)
+        return y
+
+    def apply_op(self, x):
+        """applyOp (BelosLinearProblem.hpp:1075-1086)."""
+        return self._op(x)
+
+    def apply_right_prec(self, x):
+        """applyRightPrec (BelosLinearProblem.hpp:1103-1114)."""
+        if self.RP is not None:
+            return self._prec(self.RP, x)
+        return 1.0 * x + 0.0 * x
+
     def set_problem(self):
-        """setProblem (BelosLinearProblem.hpp:836-946): R0 = B - A X; PR0 = R0."""
-        R = self.apply(self.X)
-        self.R0 = self.B - R
-        self.PR0 = self.R0
+        """setProblem (BelosLinearProblem.hpp:836-946): R0 = B - A X; PR0 = M_L R0."""
+        R = self._op(self.X)
+        self.R0 = (-1.0 * R) + (1.0 * self.B)
+        self.PR0 = self._prec(self.LP, self.R0) if self.LP is not None else self.R0
         return True
 
     def set_ls_index(self, idx):
@@ -260,9 +286,11 @@ class LinearProblem:
         return self.curB
 
     def update_solution(self, update, update_lp):
-        """updateSolution (BelosLinearProblem.hpp:743-812), no right preconditioner."""
+        """updateSolution (BelosLinearProblem.hpp:743-812): X + M_R update."""
         if update is None:
             return self.curX
+        if self.RP is not None:
+            update = self._prec(self.RP, update)
         if update_lp:
             self.curX = self.curX + update
             return self.curX
@@ -271,8 +299,30 @@ class LinearProblem:
     def curr_res_vec(self, Xs=None):
         """computeCurrResVec (BelosLinearProblem.hpp:1196-1231): R = B - A X."""
         Xs = self.curX if Xs is None else Xs
-        R = self.apply(Xs)
+        R = self._op(Xs)
         return (-1.0 * R) + (1.0 * self.curB)
+
+    def curr_prec_res_vec(self, Xs=None):
+        """computeCurrPrecResVec (BelosLinearProblem.hpp:1117-1195): M_L (B - A X)."""
+        R = self.curr_res_vec(Xs)
+        return self._prec(self.LP, R) if self.LP is not None else R
+
+
+def _scale_vector(lp, scale_type):
+    """firstCallCheckStatusSetup scaling (BelosStatusTestGenResNorm.hpp:643-700,
+    BelosStatusTestImpResNorm.hpp:815-845); None for "None" (divide by scalevalue 1)."""
+    if scale_type == "Norm of RHS":
+        return np.linalg.norm(lp.B, axis=0)
+    if scale_type == "Norm of Initial Residual":
+        return np.linalg.norm(lp.R0, axis=0)
+    if scale_type == "Norm of Preconditioned Initial Residual":
+        return np.linalg.norm(lp.PR0, axis=0)
+    if scale_type == "None":
+        return None
+    raise ValueError("invalid residual scaling type %r" % (scale_type,))
+
+
+SCALE_TYPES = ("Norm of Initial Residual", "Norm of Preconditioned Initial Residual", "Norm of RHS", "None")
 
 
 class StatusTestMaxIters:
@@ -294,8 +344,9 @@ class StatusTestImpResNorm:
     """StatusTestImpResNorm with scaling 'Norm of Preconditioned Initial Residual'
     (BelosStatusTestImpResNorm.hpp:492-749, 808-845)."""
 
-    def __init__(self, tol):
+    def __init__(self, tol, scale_type="Norm of Preconditioned Initial Residual"):
         self.tol = tol
+        self.scale_type = scale_type
         self.reset()
 
     def reset(self):
@@ -312,8 +363,8 @@ class StatusTestImpResNorm:
         lp = it.lp
         if self.first:
             self.first = False
-            self.scale = np.linalg.norm(lp.PR0, axis=0)
-            self.numrhs = lp.PR0.shape[1]
+            self.scale = _scale_vector(lp, self.scale_type)
+            self.numrhs = lp.B.shape[1]
             self.resvector = np.zeros(self.numrhs)
             self.testvector = np.ones(self.numrhs)
             self.cur_ls_num = lp.ls_num
@@ -332,7 +383,7 @@ class StatusTestImpResNorm:
                 self.resvector[p] = res[i]
         for p in self.cur_idx:
             if p != -1:
-                s = self.scale[p]
+                s = 0.0 if self.scale is None else self.scale[p]
                 self.testvector[p] = self.resvector[p] / s / 1.0 if s != 0.0 else self.resvector[p] / 1.0
         ind, lcl = [], []
         for i, p in enumerate(self.cur_idx):
@@ -356,7 +407,7 @@ class StatusTestImpResNorm:
             tmp_res = np.linalg.norm(cur_res, axis=0)
             tmp_test = []
             for i in range(have):
-                s = self.scale[ind[i]]
+                s = 0.0 if self.scale is None else self.scale[ind[i]]
                 tmp_test.append(tmp_res[lcl[i]] / s / 1.0 if s != 0.0 else tmp_res[lcl[i]] / 1.0)
             have2 = 0
             for i in range(have):
@@ -377,6 +428,106 @@ class StatusTestImpResNorm:
         need = self.cur_num_rhs
         self.status = have >= need
         return self.status
+
+
+class StatusTestGenResNorm:
+    """StatusTestGenResNorm, implicit (native residuals) or explicit (||B - A X||) form
+    (BelosStatusTestGenResNorm.hpp:455-600, 643-700).  No loss-of-accuracy check."""
+
+    loss = False
+
+    def __init__(self, tol, explicit=False, scale_type="Norm of Preconditioned Initial Residual"):
+        self.tol = tol
+        self.explicit = explicit
+        self.scale_type = scale_type
+        self.reset()
+
+    def reset(self):
+        self.status = None
+        self.first = True
+        self.cur_soln = None
+        self.cur_ls_num = 0
+        self.n_explicit = 0
+        self.testvector = None
+
+    def check(self, it):
+        lp = it.lp
+        if self.first:
+            self.first = False
+            self.scale = _scale_vector(lp, self.scale_type)
+            self.numrhs = lp.B.shape[1]
+            self.resvector = np.zeros(self.numrhs)
+            self.testvector = np.ones(self.numrhs)
+            self.cur_ls_num = lp.ls_num
+            self.cur_idx = list(lp.ls_idx)
+            self.cur_num_rhs = sum(1 for i in self.cur_idx if 0 <= i < self.numrhs)
+        if self.cur_ls_num != lp.ls_num:
+            self.cur_ls_num = lp.ls_num
+            self.cur_idx = list(lp.ls_idx)
+            self.cur_num_rhs = sum(1 for i in self.cur_idx if 0 <= i < self.numrhs)
+            self.cur_soln = None
+        elif self.status:
+            return self.status
+        if self.explicit:
+            self.n_explicit += 1
+            upd = it.current_update()
+            self.cur_soln = lp.update_solution(upd, False)
+            res = np.linalg.norm(lp.curr_res_vec(self.cur_soln), axis=0)
+        else:
+            res = it.native_residuals()
+        for i, p in enumerate(self.cur_idx):
+            if p != -1:
+                self.resvector[p] = res[i]
+        for p in self.cur_idx:
+            if p != -1:
+                s = 0.0 if self.scale is None else self.scale[p]
+                self.testvector[p] = self.resvector[p] / s / 1.0 if s != 0.0 else self.resvector[p] / 1.0
+        have = 0
+        for p in self.cur_idx:
+            if p == -1:
+                continue
+            tv = self.testvector[p]
+            if tv > self.tol:
+                pass
+            elif tv <= self.tol:
+                have += 1
+            else:
+                self.status = False
+                raise FloatingPointError("StatusTestGenResNorm: NaN detected")
+        self.status = have >= self.cur_num_rhs
+        return self.status
+
+
+class StatusTestSeq:
+    """StatusTestCombo SEQ: later members are checked only when the earlier ones pass
+    (BelosStatusTestCombo.hpp:360-380)."""
+
+    loss = False
+
+    def __init__(self, *tests):
+        self.tests = tests
+        self.status = None
+
+    @property
+    def testvector(self):
+        return self.tests[0].testvector
+
+    @property
+    def n_explicit(self):
+        return sum(t.n_explicit for t in self.tests)
+
+    def reset(self):
+        for t in self.tests:
+            t.reset()
+        self.status = None
+
+    def check(self, it):
+        for t in self.tests:
+            if not t.check(it):
+                self.status = False
+                return False
+        self.status = True
+        return True
 
 
 class StatusTestOr:
@@ -530,6 +681,50 @@ class BlockGmresIter:
             self.cur_dim = dim + k
 
 
+class BlockFGmresIter(BlockGmresIter):
+    """BelosBlockFGmresIter.hpp: flexible Block GMRES.  Z keeps the preconditioned basis
+    (Z_j = M_R V_j, :645-740); the update is Z y (:488-523).  updateLSQR is the same
+    Householder/Givens update as BlockGmresIter (:750-825)."""
+
+    def __init__(self, lp, stest, ortho, k, nb):
+        super().__init__(lp, stest, ortho, k, nb)
+        self.Z = np.zeros_like(self.V)
+
+    def current_update(self):
+        c, k = self.cur_dim, self.k
+        if c == 0:
+            return None
+        y = self.z[:c, :k].copy()
+        Rc = self.R[:c, :c]
+        for i in range(c - 1, -1, -1):
+            if i + 1 < c:
+                y[i, :] -= Rc[i, i + 1:c] @ y[i + 1:c, :]
+            y[i, :] /= Rc[i, i]
+        return self.Z[:, :c] @ y
+
+    def iterate(self):
+        k = self.k
+        search = k * self.nb
+        while (not self.stest.check(self)) and self.cur_dim + k <= search:
+            self.num_iters += 1
+            lcl = self.cur_dim + k
+            c = self.cur_dim
+            self.Z[:, c:c + k] = self.lp.apply_right_prec(self.V[:, c:c + k])
+            self.V[:, lcl:lcl + k] = self.lp.apply_op(self.Z[:, c:c + k])
+            Vnext = self.V[:, lcl:lcl + k].copy()
+            Q = self.V[:, :lcl]
+            subH = np.zeros((lcl, k))
+            subH2 = np.zeros((k, k))
+            rank = self.ortho.project_and_normalize(Vnext, Q, subH, subH2)
+            self.V[:, lcl:lcl + k] = Vnext
+            self.R[:lcl, c:c + k] = subH
+            self.R[lcl:lcl + k, c:c + k] = subH2
+            if rank != k:
+                raise OrthoFailure("couldn't generate basis of full rank")
+            self.update_lsqr()
+            self.cur_dim += k
+
+
 def _rotg(a, b):
     """BLAS drotg (reference algorithm): returns (r, c, s)."""
     roe = a if abs(a) > abs(b) else b
@@ -541,16 +736,19 @@ def _rotg(a, b):
     return r, a / r, b / r
 
 
-DEFAULTS = {
+DEFAULTS = {   # BelosBlockGmresSolMgr.hpp:317-335
     "Convergence Tolerance": 1e-8, "Maximum Restarts": 20, "Maximum Iterations": 1000,
     "Num Blocks": 300, "Block Size": 1, "Adaptive Block Size": True,
-    "Orthogonalization": "DGKS",
+    "Orthogonalization": "DGKS", "Flexible Gmres": False, "Explicit Residual Test": False,
+    "Implicit Residual Scaling": "Norm of Preconditioned Initial Residual",
+    "Explicit Residual Scaling": "Norm of Initial Residual",
 }
 
 
 class BlockGmresSolMgr:
-    """BlockGmresSolMgr::solve (BelosBlockGmresSolMgr.hpp:916-1303), non-flexible,
-    implicit residual test with loss-of-accuracy check (ImpResNorm OR MaxIters)."""
+    """BlockGmresSolMgr::solve (BelosBlockGmresSolMgr.hpp:916-1303), plain and flexible
+    ("Flexible Gmres", BlockFGmresIter); status tests as checkStatusTest (:807-903):
+    MaxIters OR (ImpResNorm | GenResNorm implicit | SEQ(implicit, explicit))."""
 
     def __init__(self, lp, params):
         p = dict(DEFAULTS)
@@ -565,12 +763,34 @@ class BlockGmresSolMgr:
         else:
             raise ValueError("oracle supports ICGS and DGKS")
 
+    def _status_tests(self, tol):
+        """checkStatusTest (BelosBlockGmresSolMgr.hpp:807-903)."""
+        p, lp = self.p, self.lp
+        self.flexible = bool(p["Flexible Gmres"])
+        exp_test = bool(p["Explicit Residual Test"])
+        if self.flexible and lp.RP is None:
+            self.flexible = False
+            if lp.LP is not None:
+                raise ValueError("flexible GMRES needs a right, not a left, preconditioner")
+        if lp.LP is not None and not self.flexible:
+            exp_test = True
+        self.exp_test = exp_test
+        imp_scale, exp_scale = p["Implicit Residual Scaling"], p["Explicit Residual Scaling"]
+        if exp_test:
+            self.imp = StatusTestGenResNorm(tol, False, imp_scale)
+            self.exp = StatusTestGenResNorm(tol, True, exp_scale)
+            self.conv = StatusTestSeq(self.imp, self.exp)
+        else:
+            self.imp = (StatusTestGenResNorm(tol, False, imp_scale) if self.flexible
+                        else StatusTestImpResNorm(tol, imp_scale))
+            self.exp = self.conv = self.imp
+
     def solve(self):
         p, lp = self.p, self.lp
         tol = float(p["Convergence Tolerance"])
         self.max_iter_test = StatusTestMaxIters(int(p["Maximum Iterations"]))
-        self.imp = StatusTestImpResNorm(tol)
-        self.stest = StatusTestOr(self.max_iter_test, self.imp)
+        self._status_tests(tol)
+        self.stest = StatusTestOr(self.max_iter_test, self.conv)
         block = int(p["Block Size"])
         nb_param = int(p["Num Blocks"])
         max_restarts = int(p["Maximum Restarts"])
@@ -595,11 +815,11 @@ class BlockGmresSolMgr:
                 nb = dim // block if block == 1 else (dim - block) // block
             else:
                 nb = nb_param
-            it = BlockGmresIter(lp, self.stest, self.ortho, block, nb)
-            if idx[-1] == -1:
-                V0 = lp.curr_res_vec()
+            it = (BlockFGmresIter if self.flexible else BlockGmresIter)(lp, self.stest, self.ortho, block, nb)
+            if self.flexible:
+                V0 = lp.curr_res_vec() if idx[-1] == -1 else lp.R0[:, idx].copy()
             else:
-                V0 = lp.PR0[:, idx].copy()
+                V0 = lp.curr_prec_res_vec() if idx[-1] == -1 else lp.PR0[:, idx].copy()
             z0 = np.zeros((block, block))
             rank = self.ortho.normalize(V0, z0)
             if rank != block:
@@ -609,8 +829,8 @@ class BlockGmresSolMgr:
             while True:
                 try:
                     it.iterate()
-                    if self.imp.status:
-                        if self.imp.loss:
+                    if self.conv.status:
+                        if self.exp.loss:
                             self.loa = True
                             converged = False
                         break
@@ -623,8 +843,13 @@ class BlockGmresSolMgr:
                             break
                         restarts += 1
                         upd = it.current_update()
-                        lp.update_solution(upd, True)
-                        V0 = lp.curr_res_vec()
+                        if self.flexible:
+                            if upd is not None:
+                                lp.curX = 1.0 * lp.curX + 1.0 * upd
+                            V0 = lp.curr_res_vec()
+                        else:
+                            lp.update_solution(upd, True)
+                            V0 = lp.curr_prec_res_vec()
                         z0 = np.zeros((block, block))
                         rank = self.ortho.normalize(V0, z0)
                         if rank != block:
@@ -634,16 +859,20 @@ class BlockGmresSolMgr:
                         raise RuntimeError("invalid return from iterate()")
                 except OrthoFailure:
                     if block != 1:
-                        if not self.imp.status:
+                        if not self.conv.status:
                             converged = False
                         break
                     it.update_lsqr(it.cur_dim)
                     self.stest.check(it)
-                    if not self.imp.status:
+                    if not self.conv.status:
                         converged = False
                     break
-            if self.imp.cur_soln is not None:
-                lp.curX = 0.0 * self.imp.cur_soln + 1.0 * self.imp.cur_soln
+            if self.flexible:
+                upd = it.current_update()
+                if upd is not None:
+                    lp.curX = 1.0 * lp.curX + 1.0 * upd
+            elif self.exp.cur_soln is not None:
+                lp.curX = 0.0 * self.exp.cur_soln + 1.0 * self.exp.cur_soln
             else:
                 upd = it.current_update()
                 lp.update_solution(upd, True)
@@ -660,19 +889,22 @@ class BlockGmresSolMgr:
                     idx = list(range(start, start + cur_rhs)) + [-1] * (block - cur_rhs)
                 lp.set_ls_index(idx)
         self.num_iters = self.max_iter_test.n_iters
-        self.achieved_tol = float(np.max(self.imp.testvector))
+        tv = self.exp.testvector if self.exp_test else self.imp.testvector
+        if tv is None or len(tv) < 1:
+            tv = self.imp.testvector
+        self.achieved_tol = float(np.max(tv))
         self.converged = converged and not self.loa
         return self.converged
 
 
-def solve(A, B, params, X0=None):
+def solve(A, B, params, X0=None, left=None, right=None):
     """Convenience driver: returns dict with X, iterations, history, counters."""
     X0 = np.zeros_like(B) if X0 is None else X0
-    lp = LinearProblem(A, X0, B)
+    lp = LinearProblem(A, X0, B, left=left, right=right)
     lp.set_problem()
     sm = BlockGmresSolMgr(lp, params)
     ok = sm.solve()
     return dict(X=lp.X, converged=ok, iterations=sm.num_iters, achieved_tol=sm.achieved_tol,
-                loa=sm.loa, n_apply=lp.n_apply, n_explicit=sm.imp.n_explicit,
+                loa=sm.loa, n_apply=lp.n_apply, n_prec=lp.n_prec, n_explicit=sm.conv.n_explicit,
                 restarts=sm.n_restarts_total, history=np.array(sm.stest.history),
                 blk_ortho_sing=sm.ortho.counters.get("blkOrthoSing", 0))

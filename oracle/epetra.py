@@ -178,6 +178,31 @@ def laplace3d_rows(nx, ny, nz, first, nloc):
     return _pad_rows(cols, vals)
 
 
+def brick3d_rows(nx, ny, nz, first, nloc, a=26.0, off=-1.0):
+    """Galeri/Xpetra Brick3D 27-point stencil with Dirichlet truncation on every face
+    (galeri/src-xpetra/Galeri_XpetraMatrixTypes.hpp:533-630, Fill9PointStencil :738-760):
+    every in-range neighbour of the 3x3x3 cube gets `off`, the centre `a` (boundary rows
+    keep `a`).  Column order is irrelevant (FillComplete sorts each row)."""
+    g = np.arange(first, first + nloc, dtype=np.int64)
+    nxy = nx * ny
+    iz = g // nxy
+    iy = (g % nxy) // nx
+    ix = g % nx
+    cols = np.full((nloc, 27), -1, dtype=np.int64)
+    vals = np.full((nloc, 27), off)
+    c = 0
+    for dz in (-1, 0, 1):
+        for dy in (-1, 0, 1):
+            for dx in (-1, 0, 1):
+                ok = ((ix + dx >= 0) & (ix + dx < nx) & (iy + dy >= 0) & (iy + dy < ny)
+                      & (iz + dz >= 0) & (iz + dz < nz))
+                cols[:, c] = np.where(ok, g + dx + dy * nx + dz * nxy, -1)
+                if dx == 0 and dy == 0 and dz == 0:
+                    vals[:, c] = a
+                c += 1
+    return _pad_rows(cols, vals)
+
+
 # ---------------------------------------------------------------------------
 # Column map and import plan (bit-exact index maps)
 # ---------------------------------------------------------------------------

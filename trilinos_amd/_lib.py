@@ -69,7 +69,13 @@ _SIGS = {
     "migmres_icgs_normalize": [vp, P(f64), i32, P(i32)],
     "migmres_dgks_project_normalize": [vp, vp, P(f64), i32, P(f64), i32, P(i32)],
     "migmres_dgks_normalize": [vp, P(f64), i32, P(i32)],
+    "migmres_plan_galeri": [C.c_char_p, i32, i32, i32, i64, i32, P(i64), P(i64), P(f64), P(i64)],
+    "migmres_jacobi_create": [vp, i32, f64, P(vp)],
+    "migmres_prec_destroy": [vp],
+    "migmres_prec_apply": [vp, vp, vp],
+    "migmres_prec_diagonal": [vp, P(f64)],
     "migmres_solver_create": [vp, P(vp)],
+    "migmres_solver_set_prec": [vp, i32, vp],
     "migmres_solver_destroy": [vp],
     "migmres_solver_set_int": [vp, C.c_char_p, i64],
     "migmres_solver_set_double": [vp, C.c_char_p, f64],

@@ -161,11 +161,32 @@ class DGKSOrthoManager(ICGSOrthoManager):
 
 
 class LinearProblem:
-    """Belos::LinearProblem(A, X, B) without preconditioners."""
+    """Belos::LinearProblem(A, X, B) (belos/src/BelosLinearProblem.hpp) with optional
+    left/right preconditioners (setLeftPrec / setRightPrec, :170-175), e.g.
+    trilinos_amd.ifpack2.Relaxation."""
 
     def __init__(self, A, X, B):
         self.A, self.X, self.B = A, X, B
+        self.LP = self.RP = None
         self._set = False
+
+    def setLeftPrec(self, LP):
+        self.LP = LP
+
+    def setRightPrec(self, RP):
+        self.RP = RP
+
+    def getLeftPrec(self):
+        return self.LP
+
+    def getRightPrec(self):
+        return self.RP
+
+    def isLeftPrec(self):
+        return self.LP is not None
+
+    def isRightPrec(self):
+        return self.RP is not None
 
     def setProblem(self):
         if self.X is None or self.B is None or self.A is None:
@@ -181,17 +202,20 @@ class LinearProblem:
 
 _INT_PARAMS = {"Block Size", "Num Blocks", "Maximum Iterations", "Maximum Restarts", "Verbosity",
                "Output Frequency"}
-_BOOL_PARAMS = {"Adaptive Block Size"}
+_BOOL_PARAMS = {"Adaptive Block Size", "Flexible Gmres", "Explicit Residual Test"}
 _DOUBLE_PARAMS = {"Convergence Tolerance"}
-_STRING_PARAMS = {"Orthogonalization", "Implicit Residual Scaling"}
+_STRING_PARAMS = {"Orthogonalization", "Implicit Residual Scaling", "Explicit Residual Scaling"}
 
-# BelosBlockGmresSolMgr.hpp:323-338 and DefaultSolverParameters::convTol
+# BelosBlockGmresSolMgr.hpp:317-338, 438-486 and DefaultSolverParameters::convTol
 DEFAULT_PARAMETERS = {
     "Convergence Tolerance": 1e-8, "Maximum Restarts": 20, "Maximum Iterations": 1000,
     "Num Blocks": 300, "Block Size": 1, "Adaptive Block Size": True, "Verbosity": 0,
-    "Output Frequency": -1, "Orthogonalization": "DGKS",
+    "Output Frequency": -1, "Orthogonalization": "DGKS", "Flexible Gmres": False,
+    "Explicit Residual Test": False,
     "Implicit Residual Scaling": "Norm of Preconditioned Initial Residual",
+    "Explicit Residual Scaling": "Norm of Initial Residual",
 }
+SCALE_TYPES = ("Norm of Initial Residual", "Norm of Preconditioned Initial Residual", "Norm of RHS", "None")
 
 
 class BlockGmresSolMgr:
@@ -253,6 +277,8 @@ class BlockGmresSolMgr:
                 raise ValueError('"Num Blocks" must be strictly positive.')
             if k == "Orthogonalization" and v not in ("DGKS", "ICGS", "IMGS"):
                 raise ValueError('"Orthogonalization" must be either "DGKS", "ICGS", or "IMGS".')
+            if k in ("Implicit Residual Scaling", "Explicit Residual Scaling") and v not in SCALE_TYPES:
+                raise ValueError(f'invalid residual scaling type "{v}"')
             self.params[k] = v
             if self.h is not None:
                 self._push(k, v)
@@ -267,6 +293,8 @@ class BlockGmresSolMgr:
         if self.params["Orthogonalization"] not in ("ICGS", "DGKS"):
             raise NotImplementedError('device Block GMRES implements "Orthogonalization" = "ICGS" and "DGKS"')
         self._ensure()
+        for side, M in ((0, self.problem.LP), (1, self.problem.RP)):
+            call("migmres_solver_set_prec", self.h, side, M.h if M is not None else None)
         conv = C.c_int()
         call("migmres_solver_solve", self.h, self.problem.A.h, self.problem.X.h,
              self.problem.B.h, C.byref(conv))
@@ -295,9 +323,10 @@ class BlockGmresSolMgr:
         return out[:nr.value * nc.value].reshape(nr.value, nc.value)
 
     def counters(self):
-        out = (C.c_longlong * 5)()
-        call("migmres_solver_counters", self.h, out, 5)
-        keys = ("applies", "explicit_checks", "restarts", "blk_ortho_sing", "block_iterations")
+        out = (C.c_longlong * 6)()
+        call("migmres_solver_counters", self.h, out, 6)
+        keys = ("applies", "explicit_checks", "restarts", "blk_ortho_sing", "block_iterations",
+                "prec_applies")
         return dict(zip(keys, list(out)))
 
     def timers(self):

@@ -107,6 +107,11 @@ void launch_copy(hipStream_t s, MvDesc A, MvDesc Y, int nrows);
 // Epetra_MultiVector::Random semantics over global rows [first, first+nrows).
 void launch_random(hipStream_t s, MvDesc Y, int nrows, long long first, long long n_global,
                    unsigned int seed);
+// Point Jacobi: dinv = 1/diag(local CSR); Y = (omega*dinv)*X or Y = 1*Y + (omega*dinv)*X.
+void launch_diag_inv(hipStream_t s, const int *rowptr, const int *cols, const double *vals, int n,
+                     double *dinv);
+void launch_jacobi(hipStream_t s, MvDesc X, MvDesc Y, const double *dinv, double omega, int nrows,
+                   bool accumulate);
 // send[c*count + i] = X[lids[i], c]
 void launch_pack(hipStream_t s, MvDesc X, const int *lids, int count, double *send, int k);
 

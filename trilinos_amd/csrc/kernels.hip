@@ -717,6 +717,55 @@ __global__ __launch_bounds__(256) void k_pack(MvDesc X, const int *__restrict__ 
   if (i < count) send[(long long)c * count + i] = colp(X, c)[lids[i]];
 }
 
+// Point-Jacobi (Ifpack2::Relaxation "Jacobi", Ifpack2_Relaxation_def.hpp:1390-1454).
+// dinv[i] = 1 / (first entry of local row i whose local column is i; 0 if none): the owned
+// rows come first in the column map, so an owned row's diagonal has local column == row.
+__global__ __launch_bounds__(256) void k_diag_inv(const int *__restrict__ rowptr,
+                                                  const int *__restrict__ cols,
+                                                  const double *__restrict__ vals, int n,
+                                                  double *__restrict__ dinv) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= n) return;
+  double d = 0.0;
+  for (int p = rowptr[r]; p < rowptr[r + 1]; ++p)
+    if (cols[p] == r) {
+      d = vals[p];
+      break;
+    }
+  dinv[r] = 1.0 / d;
+}
+
+// Y = (omega * dinv_i) * X (first sweep from zero) or Y = 1*Y + (omega * dinv_i) * X
+// (later sweeps, X = the residual): the KokkosBlas mult expression c*C + (ab*A_i)*B,
+// each product and the sum rounded separately.
+template <bool ACC>
+__global__ __launch_bounds__(256) void k_jacobi(MvDesc X, MvDesc Y, const double *__restrict__ dinv,
+                                                double omega, int nrows) {
+#pragma clang fp contract(off)
+  const int c = blockIdx.y;
+  const long long r = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (r >= nrows) return;
+  const double t = (omega * dinv[r]) * colp(X, c)[r];
+  double *y = colp(Y, c) + r;
+  *y = ACC ? 1.0 * (*y) + t : t;
+}
+
+void launch_diag_inv(hipStream_t s, const int *rowptr, const int *cols, const double *vals, int n,
+                     double *dinv) {
+  if (n <= 0) return;
+  k_diag_inv<<<cdiv(n, 256), 256, 0, s>>>(rowptr, cols, vals, n, dinv);
+  LAUNCH_CHECK();
+}
+void launch_jacobi(hipStream_t s, MvDesc X, MvDesc Y, const double *dinv, double omega, int nrows,
+                   bool accumulate) {
+  if (nrows <= 0 || Y.ncols <= 0) return;
+  if (accumulate)
+    k_jacobi<true><<<dim3(cdiv(nrows, 256), Y.ncols), 256, 0, s>>>(X, Y, dinv, omega, nrows);
+  else
+    k_jacobi<false><<<dim3(cdiv(nrows, 256), Y.ncols), 256, 0, s>>>(X, Y, dinv, omega, nrows);
+  LAUNCH_CHECK();
+}
+
 void launch_axpby(hipStream_t s, double alpha, MvDesc A, double beta, MvDesc B, MvDesc Y, int nrows) {
   if (nrows <= 0 || Y.ncols <= 0) return;
   k_axpby<<<dim3(cdiv(nrows, 256), Y.ncols), 256, 0, s>>>(alpha, A, beta, B, Y, nrows);

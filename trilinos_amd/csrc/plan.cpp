@@ -151,10 +151,34 @@ void local_crs(int n_local, const long long *rowptr, const long long *gcols, con
 
 // Galeri Cross2D / Cross3D rows in InsertGlobalValues order
 // (galeri/src-epetra/CrsMatrices/Galeri_Cross2D.h, Galeri_Cross3D.h:78-128;
-// neighbours: galeri/src-epetra/Galeri_Utils.cpp:331-398).
+// neighbours: galeri/src-epetra/Galeri_Utils.cpp:331-398); "Brick3D" is the 27-point
+// Xpetra Brick3D (galeri/src-xpetra/Galeri_XpetraMatrixTypes.hpp:533-630) with a = 26,
+// b..g = -1 and Dirichlet truncation on every face (boundary rows keep 26).
 void galeri_rows(const std::string &kind, int nx, int ny, int nz, long long first, int n_local,
                  std::vector<long long> &rowptr, std::vector<long long> &gcols,
                  std::vector<double> &vals) {
+  if (kind == "Brick3D") {
+    const long long nxy = (long long)nx * ny;
+    rowptr.assign((size_t)n_local + 1, 0);
+    gcols.clear();
+    vals.clear();
+    gcols.reserve((size_t)n_local * 27);
+    vals.reserve((size_t)n_local * 27);
+    for (int r = 0; r < n_local; ++r) {
+      const long long g = first + r;
+      const long long iz = g / nxy, iy = (g % nxy) / nx, ix = g % nx;
+      for (int dz = -1; dz <= 1; ++dz)
+        for (int dy = -1; dy <= 1; ++dy)
+          for (int dx = -1; dx <= 1; ++dx) {
+            if (ix + dx < 0 || ix + dx >= nx || iy + dy < 0 || iy + dy >= ny || iz + dz < 0 || iz + dz >= nz)
+              continue;
+            gcols.push_back(g + dx + dy * (long long)nx + dz * nxy);
+            vals.push_back(dx == 0 && dy == 0 && dz == 0 ? 26.0 : -1.0);
+          }
+      rowptr[(size_t)r + 1] = (long long)gcols.size();
+    }
+    return;
+  }
   const bool three = kind == "Laplace3D";
   if (!three && kind != "Laplace2D") throw Error(MIGMRES_EINVAL, "unknown Galeri matrix " + kind);
   const long long nxy = (long long)nx * ny;

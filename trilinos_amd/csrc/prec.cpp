@@ -1,0 +1,79 @@
+// Point-Jacobi preconditioner on the device: Ifpack2::Relaxation with "relaxation: type" =
+// "Jacobi" (ifpack2/src/Ifpack2_Relaxation_def.hpp; compute() :990-1270 keeps the
+// reciprocal of the diagonal, ApplyInverseJacobi :1390-1454 applies it), the
+// right/left preconditioner of config 5.
+#include "runtime.h"
+
+using namespace migmres;
+
+migmres_prec::~migmres_prec() {
+  if (d_dinv) hipFree(d_dinv);
+  delete work;
+}
+
+namespace migmres {
+
+// Y = M X.  Zero starting solution: the first sweep is Y = (omega d^-1) X; every further
+// sweep forms R = X - A Y (SpMM with alpha = -1, beta = 1 on a copy of X: y - sum, the
+// Tpetra::Details::residual expression) and Y = 1*Y + (omega d^-1) R.
+void prec_apply(migmres_prec &M, const migmres_mv &X, migmres_mv &Y) {
+  MIG_CHECK(X.ncols == Y.ncols, "Jacobi apply: X and Y column counts differ");
+  MIG_CHECK(X.n_local == M.A->n_local && Y.n_local == M.A->n_local, "Jacobi apply: row map mismatch");
+  MIG_CHECK(X.base != Y.base || X.ncols == 0, "Jacobi apply: X and Y must not alias");
+  migmres_ctx *c = M.ctx;
+  const int n = M.A->n_local;
+  {
+    ProfScope ps(c, K_AXPBY, 8.0 * n * (2.0 * X.ncols + 1.0));
+    launch_jacobi(c->stream, X.desc(), Y.desc(), M.d_dinv, M.damping, n, false);
+  }
+  if (M.sweeps > 1) {
+    if (!M.work || M.work->ncols != X.ncols) {
+      delete M.work;
+      M.work = mv_create(c, X.n_global, X.n_local, X.ncols);
+    }
+    for (int j = 1; j < M.sweeps; ++j) {
+      mv_assign(X, *M.work);
+      crs_apply(*M.A, Y, *M.work, -1.0, 1.0);
+      ProfScope ps(c, K_AXPBY, 8.0 * n * (3.0 * X.ncols + 1.0));
+      launch_jacobi(c->stream, M.work->desc(), Y.desc(), M.d_dinv, M.damping, n, true);
+    }
+  }
+  ++M.n_apply;
+}
+
+}  // namespace migmres
+
+extern "C" int migmres_jacobi_create(migmres_crs *A, int sweeps, double damping, migmres_prec **out) {
+  return guard([&] {
+    MIG_CHECK(A && out, "jacobi_create: null argument");
+    MIG_CHECK(sweeps >= 1, "\"relaxation: sweeps\" must be >= 1");
+    auto *M = new migmres_prec();
+    M->ctx = A->ctx;
+    M->A = A;
+    M->sweeps = sweeps;
+    M->damping = damping;
+    const int n = A->n_local;
+    MIG_HIP(hipMalloc(&M->d_dinv, sizeof(double) * (n > 0 ? n : 1)));
+    launch_diag_inv(A->ctx->stream, A->d_rowptr, A->d_cols, A->d_vals, n, M->d_dinv);
+    MIG_HIP(hipStreamSynchronize(A->ctx->stream));
+    *out = M;
+  });
+}
+
+extern "C" int migmres_prec_destroy(migmres_prec *M) {
+  return guard([&] { delete M; });
+}
+
+extern "C" int migmres_prec_apply(migmres_prec *M, const migmres_mv *X, migmres_mv *Y) {
+  return guard([&] {
+    MIG_CHECK(M && X && Y, "prec_apply: null argument");
+    prec_apply(*M, *X, *Y);
+  });
+}
+
+extern "C" int migmres_prec_diagonal(const migmres_prec *M, double *dinv_out) {
+  return guard([&] {
+    MIG_CHECK(M && dinv_out, "prec_diagonal: null argument");
+    MIG_HIP(hipMemcpy(dinv_out, M->d_dinv, sizeof(double) * M->A->n_local, hipMemcpyDeviceToHost));
+  });
+}

@@ -937,7 +937,7 @@ extern "C" int migmres_crs_create_galeri(migmres_ctx *ctx, const char *kind, int
                                          migmres_crs **out) {
   return guard([&] {
     const std::string k(kind ? kind : "");
-    const long long n_global = (long long)nx * ny * (k == "Laplace3D" ? nz : 1);
+    const long long n_global = (long long)nx * ny * (k == "Laplace3D" || k == "Brick3D" ? nz : 1);
     long long first = 0;
     int n_local = 0;
     uniform_map(n_global, ctx->nranks, ctx->rank, &first, &n_local);
@@ -945,6 +945,21 @@ extern "C" int migmres_crs_create_galeri(migmres_ctx *ctx, const char *kind, int
     std::vector<double> v;
     galeri_rows(k, nx, ny, nz, first, n_local, rp, gc, v);
     *out = crs_create(ctx, n_global, first, n_local, rp.data(), gc.data(), v.data());
+  });
+}
+
+extern "C" int migmres_plan_galeri(const char *kind, int nx, int ny, int nz, long long first, int n_local,
+                                   long long *rowptr_out, long long *gcols_out, double *vals_out,
+                                   long long *nnz_out) {
+  return guard([&] {
+    MIG_CHECK(kind && nnz_out, "plan_galeri: null argument");
+    std::vector<long long> rp, gc;
+    std::vector<double> v;
+    galeri_rows(kind, nx, ny, nz, first, n_local, rp, gc, v);
+    *nnz_out = (long long)gc.size();
+    if (rowptr_out) std::memcpy(rowptr_out, rp.data(), sizeof(long long) * rp.size());
+    if (gcols_out) std::memcpy(gcols_out, gc.data(), sizeof(long long) * gc.size());
+    if (vals_out) std::memcpy(vals_out, v.data(), sizeof(double) * v.size());
   });
 }
 

@@ -142,7 +142,22 @@ struct migmres_crs {
   ~migmres_crs();
 };
 
+// Point-Jacobi preconditioner (Ifpack2::Relaxation "Jacobi"): Y = M X with `sweeps`
+// sweeps from a zero start, damping `damping` (see prec.cpp).
+struct migmres_prec {
+  migmres_ctx *ctx = nullptr;
+  migmres_crs *A = nullptr;
+  double *d_dinv = nullptr;
+  int sweeps = 1;
+  double damping = 1.0;
+  long long n_apply = 0;
+  migmres_mv *work = nullptr;  // residual scratch for sweeps > 1
+  ~migmres_prec();
+};
+
 namespace migmres {
+
+void prec_apply(migmres_prec &M, const migmres_mv &X, migmres_mv &Y);
 
 migmres_mv *mv_create(migmres_ctx *ctx, long long n_global, int n_local, int ncols);
 migmres_mv *mv_view(migmres_mv *parent, const int *idx, int n);

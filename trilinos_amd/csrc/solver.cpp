@@ -595,7 +595,11 @@ struct Params {
   int num_blocks = 300;
   int block_size = 1;
   bool adaptive = true;
+  bool flexible = false;
+  bool exp_res_test = false;
   std::string ortho = "DGKS";
+  std::string imp_scale = "Norm of Preconditioned Initial Residual";
+  std::string exp_scale = "Norm of Initial Residual";
   int verbosity = 0;
   int output_freq = -1;
 };
@@ -608,6 +612,7 @@ struct Params {
 struct migmres_solver {
   migmres_ctx *ctx = nullptr;
   Params p;
+  migmres_prec *left = nullptr, *right = nullptr;  // borrowed (setLeftPrec / setRightPrec)
   Icgs ortho;
   FastIcgs fast;
   bool use_fast = true;
@@ -617,7 +622,7 @@ struct migmres_solver {
   bool loa = false;
   std::vector<double> history;
   int hist_cols = 0;
-  long long n_apply = 0, n_explicit = 0, n_restarts = 0, n_block_iters = 0;
+  long long n_apply = 0, n_explicit = 0, n_restarts = 0, n_block_iters = 0, n_prec = 0;
   double t_total = 0, t_spmm = 0, t_ortho = 0, t_lsq = 0, t_comm = 0;
   double t_check = 0, t_restart = 0, t_setup = 0;
   bool sync_timers() const { return (p.verbosity & 1) != 0; }
@@ -628,16 +633,25 @@ namespace {
 using Clock = std::chrono::steady_clock;
 double since(Clock::time_point t0) { return std::chrono::duration<double>(Clock::now() - t0).count(); }
 
-struct Problem {  // LinearProblem without preconditioners
+// LinearProblem (BelosLinearProblem.hpp) with optional left/right preconditioners.
+struct Problem {
   migmres_solver *S;
   migmres_crs *A;
   migmres_mv *X, *B;
-  MvPtr R0;  // PR0 == R0
+  migmres_prec *LP = nullptr, *RP = nullptr;
+  MvPtr R0, PR0;  // PR0 empty: PR0 == R0 (no left preconditioner)
+  MvPtr tmp;      // scratch of apply()
   std::vector<int> ls_idx, cur;
   int ls_num = 0;
   MvPtr curX, curB;
 
-  void apply(const migmres_mv &x, migmres_mv &y) {
+  migmres_mv &pr0() { return PR0.p ? *PR0 : *R0; }
+  MvPtr clone(int k) { return MvPtr(mv_create(X->ctx, X->n_global, X->n_local, k)); }
+  migmres_mv &scratch(int k) {
+    if (!tmp.p || tmp->ncols != k) tmp = clone(k);
+    return *tmp;
+  }
+  void op(const migmres_mv &x, migmres_mv &y) {  // OPT::Apply(A)
     auto t0 = Clock::now();
     crs_apply(*A, x, y, 1.0, 0.0);
     ++S->n_apply;
@@ -646,10 +660,45 @@ struct Problem {  // LinearProblem without preconditioners
       S->t_spmm += since(t0);
     }
   }
+  void prec(migmres_prec &M, const migmres_mv &x, migmres_mv &y) {
+    prec_apply(M, x, y);
+    ++S->n_prec;
+  }
+  // apply (BelosLinearProblem.hpp:989-1072): y = M_L A M_R x
+  void apply(const migmres_mv &x, migmres_mv &y) {
+    if (!LP && !RP) {
+      op(x, y);
+    } else if (LP && RP) {
+      migmres_mv &t = scratch(y.ncols);
+      prec(*RP, x, y);
+      op(y, t);
+      prec(*LP, t, y);
+    } else if (LP) {
+      migmres_mv &t = scratch(y.ncols);
+      op(x, t);
+      prec(*LP, t, y);
+    } else {
+      migmres_mv &t = scratch(y.ncols);
+      prec(*RP, x, t);
+      op(t, y);
+    }
+  }
+  // applyRightPrec (BelosLinearProblem.hpp:1103-1114)
+  void apply_right_prec(const migmres_mv &x, migmres_mv &y) {
+    if (RP)
+      prec(*RP, x, y);
+    else
+      mv_add_mv(1.0, x, 0.0, x, y);
+  }
   void set_problem() {  // setProblem (BelosLinearProblem.hpp:836-946)
-    R0 = MvPtr(mv_create(X->ctx, X->n_global, X->n_local, X->ncols));
-    apply(*X, *R0);
+    R0 = clone(X->ncols);
+    op(*X, *R0);
     mv_add_mv(-1.0, *R0, 1.0, *B, *R0);
+    PR0.reset();
+    if (LP) {
+      PR0 = clone(X->ncols);
+      prec(*LP, *R0, *PR0);
+    }
   }
   unsigned int aug_seed = 20250219u;  // MvRandom stream for augmented right-hand sides
   std::vector<int> vld, newi;
@@ -696,27 +745,67 @@ struct Problem {  // LinearProblem without preconditioners
     mv_assign(*src, *dst);
     MIG_HIP(hipStreamSynchronize(X->ctx->stream));
   }
+  // updateSolution(update, updateLP = true) (BelosLinearProblem.hpp:743-812): X += M_R update
+  void update_solution(const MvPtr &upd) {
+    if (!upd.p) return;
+    if (RP) {
+      MvPtr ru = clone(upd->ncols);
+      prec(*RP, *upd, *ru);
+      mv_add_mv(1.0, *curX, 1.0, *ru, *curX);
+    } else {
+      mv_add_mv(1.0, *curX, 1.0, *upd, *curX);
+    }
+  }
+  // updateSolution(update, updateLP = false): out = X + M_R update (X itself when no update)
+  void updated_solution(const MvPtr &upd, migmres_mv &out) {
+    if (!upd.p) {
+      mv_assign(*curX, out);
+    } else if (RP) {
+      MvPtr ru = clone(upd->ncols);
+      prec(*RP, *upd, *ru);
+      mv_add_mv(1.0, *curX, 1.0, *ru, out);
+    } else {
+      mv_add_mv(1.0, *curX, 1.0, *upd, out);
+    }
+  }
   // computeCurrResVec: R = B - A*Xs (BelosLinearProblem.hpp:1196-1231)
   void curr_res_vec(migmres_mv &R, const migmres_mv *Xs = nullptr) {
-    apply(Xs ? *Xs : *curX, R);
+    op(Xs ? *Xs : *curX, R);
     mv_add_mv(-1.0, R, 1.0, *curB, R);
+  }
+  // computeCurrPrecResVec: R = M_L (B - A*X) (BelosLinearProblem.hpp:1117-1195)
+  void curr_prec_res_vec(migmres_mv &R) {
+    if (!LP) {
+      curr_res_vec(R);
+      return;
+    }
+    MvPtr t = clone(R.ncols);
+    curr_res_vec(*t);
+    prec(*LP, *t, R);
   }
 };
 
-struct ImpResNorm {  // StatusTestImpResNorm, scaling "Norm of Preconditioned Initial Residual"
+// Residual status tests: StatusTestImpResNorm (implicit with the explicit confirmation and
+// loss-of-accuracy logic, BelosStatusTestImpResNorm.hpp:492-749) and StatusTestGenResNorm
+// (implicit or explicit form, BelosStatusTestGenResNorm.hpp:455-600).
+struct ResTest {
+  enum Kind { IMP_RES_NORM, GEN_IMPLICIT, GEN_EXPLICIT } kind;
+  std::string scale_type;
   double tol, curr_tol;
   bool first = true, loss = false, passed = false;
   int cur_ls_num = 0, numrhs = 0, cur_num_rhs = 0;
+  long long n_explicit = 0;
   std::vector<int> cur_idx;
   std::vector<double> scale, resvector, testvector;
   MvPtr cur_soln;
   bool have_soln = false;
-  explicit ImpResNorm(double t) : tol(t), curr_tol(t) {}
+  ResTest(Kind k, double t, const std::string &st) : kind(k), scale_type(st), tol(t), curr_tol(t) {}
 };
 
-struct Iter {  // BlockGmresIter state (keepHessenberg = false: H and R share storage)
+struct Iter {  // BlockGmresIter / BlockFGmresIter state (H and R share storage)
   int k, nb, sd, cur_dim = 0, num_iters = 0;
   MvPtr V;
+  MvPtr Z;  // flexible: Z_j = M_R V_j (BelosBlockFGmresIter.hpp:316)
   std::vector<double> R, z, beta, cs, sn;
   int ldr() const { return sd; }
   double &Rat(int i, int j) { return R[(size_t)i + (size_t)j * sd]; }
@@ -726,12 +815,33 @@ struct Iter {  // BlockGmresIter state (keepHessenberg = false: H and R share st
 struct Engine {
   migmres_solver *S;
   Problem lp;
-  ImpResNorm imp;
+  // checkStatusTest (BelosBlockGmresSolMgr.hpp:807-903): conv = imp, or SEQ(imp, exp)
+  ResTest imp, exp;
+  bool seq = false, flexible = false;
+  bool conv_passed = false;
   int max_iters;
   int mi_n_iters = 0;
   bool mi_passed = false;
 
-  Engine(migmres_solver *s, double tol, int mi) : S(s), imp(tol), max_iters(mi) {}
+  Engine(migmres_solver *s, double tol, int mi)
+      : S(s), imp(ResTest::IMP_RES_NORM, tol, s->p.imp_scale), exp(ResTest::GEN_EXPLICIT, tol, s->p.exp_scale),
+        max_iters(mi) {}
+  ResTest &exp_conv() { return seq ? exp : imp; }
+
+  void setup_status_tests(bool has_left, bool has_right) {
+    flexible = S->p.flexible;
+    bool exp_test = S->p.exp_res_test;
+    if (flexible && !has_right) {
+      flexible = false;
+      MIG_CHECK(!has_left, "BlockGmresSolMgr: flexible GMRES needs a right, not a left, preconditioner");
+    }
+    if (has_left && !flexible) exp_test = true;
+    seq = exp_test;
+    if (seq)
+      imp.kind = ResTest::GEN_IMPLICIT;
+    else
+      imp.kind = flexible ? ResTest::GEN_IMPLICIT : ResTest::IMP_RES_NORM;
+  }
 
   std::vector<double> native_residuals(Iter &it) {  // getNativeResiduals
     std::vector<double> r((size_t)it.k);
@@ -769,7 +879,7 @@ struct Engine {
         y[(size_t)i + (size_t)j * c] = t / it.Rat(i, i);
       }
     MvPtr upd(mv_create(lp.X->ctx, lp.X->n_global, lp.X->n_local, k));
-    MvPtr Vc = view(*it.V, 0, c);
+    MvPtr Vc = view(it.Z.p ? *it.Z : *it.V, 0, c);  // BlockFGmresIter: Z y (:488-523)
     mv_times_mat_add_mv(1.0, *Vc, y.data(), c, 0.0, *upd);
     return upd;
   }
@@ -780,91 +890,113 @@ struct Engine {
     return mi_passed;
   }
 
-  bool imp_check(Iter &it) {  // StatusTestImpResNorm::checkStatus
-    if (imp.first) {
-      imp.first = false;
-      imp.numrhs = lp.R0->ncols;
-      imp.scale.assign((size_t)imp.numrhs, 0.0);
-      mv_norm(*lp.R0, imp.scale.data(), MIGMRES_TWO_NORM);
-      imp.resvector.assign((size_t)imp.numrhs, 0.0);
-      imp.testvector.assign((size_t)imp.numrhs, 1.0);
-      imp.cur_ls_num = lp.ls_num;
-      imp.cur_idx = lp.ls_idx;
-      imp.cur_num_rhs = 0;
-      for (int i : imp.cur_idx)
-        if (i > -1 && i < imp.numrhs) ++imp.cur_num_rhs;
+  // firstCallCheckStatusSetup scaling (GenResNorm :643-700, ImpResNorm :815-845)
+  void scale_setup(ResTest &t) {
+    t.numrhs = lp.B->ncols;
+    t.scale.clear();
+    if (t.scale_type == "None") return;
+    t.scale.assign((size_t)t.numrhs, 0.0);
+    if (t.scale_type == "Norm of RHS")
+      mv_norm(*lp.B, t.scale.data(), MIGMRES_TWO_NORM);
+    else if (t.scale_type == "Norm of Initial Residual")
+      mv_norm(*lp.R0, t.scale.data(), MIGMRES_TWO_NORM);
+    else
+      mv_norm(lp.pr0(), t.scale.data(), MIGMRES_TWO_NORM);
+  }
+  double scaled(const ResTest &t, int p, double r) const {
+    const double s = t.scale.empty() ? 0.0 : t.scale[(size_t)p];
+    return s != 0.0 ? r / s / 1.0 : r / 1.0;
+  }
+
+  bool res_check(ResTest &t, Iter &it) {
+    if (t.first) {
+      t.first = false;
+      scale_setup(t);
+      t.resvector.assign((size_t)t.numrhs, 0.0);
+      t.testvector.assign((size_t)t.numrhs, 1.0);
+      t.cur_ls_num = lp.ls_num;
+      t.cur_idx = lp.ls_idx;
+      t.cur_num_rhs = 0;
+      for (int i : t.cur_idx)
+        if (i > -1 && i < t.numrhs) ++t.cur_num_rhs;
     }
-    if (imp.cur_ls_num != lp.ls_num) {
-      imp.cur_ls_num = lp.ls_num;
-      imp.cur_idx = lp.ls_idx;
-      imp.cur_num_rhs = 0;
-      for (int i : imp.cur_idx)
-        if (i > -1 && i < imp.numrhs) ++imp.cur_num_rhs;
-      imp.have_soln = false;
-    } else if (imp.passed) {
+    if (t.cur_ls_num != lp.ls_num) {
+      t.cur_ls_num = lp.ls_num;
+      t.cur_idx = lp.ls_idx;
+      t.cur_num_rhs = 0;
+      for (int i : t.cur_idx)
+        if (i > -1 && i < t.numrhs) ++t.cur_num_rhs;
+      t.have_soln = false;
+    } else if (t.passed) {
       return true;
     }
-    auto res = native_residuals(it);
-    for (size_t i = 0; i < imp.cur_idx.size(); ++i)
-      if (imp.cur_idx[i] != -1) imp.resvector[(size_t)imp.cur_idx[i]] = res[i];
-    for (int p : imp.cur_idx)
-      if (p != -1) {
-        const double s = imp.scale[(size_t)p];
-        imp.testvector[(size_t)p] = s != 0.0 ? imp.resvector[(size_t)p] / s / 1.0 : imp.resvector[(size_t)p] / 1.0;
-      }
+    const int k = lp.curX->ncols;
+    auto explicit_norms = [&](std::vector<double> &out) {
+      ++t.n_explicit;
+      ++S->n_explicit;
+      MvPtr upd = current_update(it);
+      if (!t.cur_soln.p || t.cur_soln->ncols != k) t.cur_soln = lp.clone(k);
+      lp.updated_solution(upd, *t.cur_soln);
+      t.have_soln = true;
+      MvPtr cur_res = lp.clone(k);
+      lp.curr_res_vec(*cur_res, t.cur_soln.p);
+      out.assign((size_t)k, 0.0);
+      mv_norm(*cur_res, out.data(), MIGMRES_TWO_NORM);
+    };
+    std::vector<double> res;
+    if (t.kind == ResTest::GEN_EXPLICIT)
+      explicit_norms(res);
+    else
+      res = native_residuals(it);
+    for (size_t i = 0; i < t.cur_idx.size(); ++i)
+      if (t.cur_idx[i] != -1) t.resvector[(size_t)t.cur_idx[i]] = res[i];
+    for (int p : t.cur_idx)
+      if (p != -1) t.testvector[(size_t)p] = scaled(t, p, t.resvector[(size_t)p]);
+    const double tol_now = t.kind == ResTest::IMP_RES_NORM ? t.curr_tol : t.tol;
     std::vector<int> ind, lcl;
-    for (size_t i = 0; i < imp.cur_idx.size(); ++i) {
-      const int p = imp.cur_idx[i];
+    for (size_t i = 0; i < t.cur_idx.size(); ++i) {
+      const int p = t.cur_idx[i];
       if (p == -1) continue;
-      const double tv = imp.testvector[(size_t)p];
-      if (tv > imp.curr_tol) {
-      } else if (tv <= imp.curr_tol) {
+      const double tv = t.testvector[(size_t)p];
+      if (tv > tol_now) {
+      } else if (tv <= tol_now) {
         ind.push_back(p);
         lcl.push_back((int)i);
       } else {
-        throw Error(MIGMRES_ESTATE, "StatusTestImpResNorm: implicit residual norm is NaN");
+        throw Error(MIGMRES_ESTATE, "residual status test: residual norm is NaN");
       }
     }
     int have = (int)ind.size();
-    if (have) {
-      ++S->n_explicit;
-      MvPtr upd = current_update(it);
-      const int k = lp.curX->ncols;
-      if (!imp.cur_soln.p || imp.cur_soln->ncols != k)
-        imp.cur_soln = MvPtr(mv_create(lp.X->ctx, lp.X->n_global, lp.X->n_local, k));
-      if (upd.p)
-        mv_add_mv(1.0, *lp.curX, 1.0, *upd, *imp.cur_soln);
-      else
-        mv_assign(*lp.curX, *imp.cur_soln);
-      imp.have_soln = true;
-      MvPtr cur_res(mv_create(lp.X->ctx, lp.X->n_global, lp.X->n_local, k));
-      lp.curr_res_vec(*cur_res, imp.cur_soln.p);
-      std::vector<double> tmp_res((size_t)k);
-      mv_norm(*cur_res, tmp_res.data(), MIGMRES_TWO_NORM);
+    if (have && t.kind == ResTest::IMP_RES_NORM) {
+      std::vector<double> tmp_res;
+      explicit_norms(tmp_res);
       std::vector<double> tmp_test((size_t)have);
-      for (int i = 0; i < have; ++i) {
-        const double s = imp.scale[(size_t)ind[(size_t)i]];
-        tmp_test[(size_t)i] = s != 0.0 ? tmp_res[(size_t)lcl[(size_t)i]] / s / 1.0 : tmp_res[(size_t)lcl[(size_t)i]] / 1.0;
-      }
+      for (int i = 0; i < have; ++i) tmp_test[(size_t)i] = scaled(t, ind[(size_t)i], tmp_res[(size_t)lcl[(size_t)i]]);
       int have2 = 0;
       for (int i = 0; i < have; ++i) {
-        if (tmp_test[(size_t)i] <= imp.tol) {
+        if (tmp_test[(size_t)i] <= t.tol) {
           ind[(size_t)have2++] = ind[(size_t)i];
         } else {
-          const double diff = std::fabs(imp.testvector[(size_t)ind[(size_t)i]] - tmp_test[(size_t)i]);
-          if (diff > imp.curr_tol) {
-            imp.loss = true;
+          const double diff = std::fabs(t.testvector[(size_t)ind[(size_t)i]] - tmp_test[(size_t)i]);
+          if (diff > t.curr_tol) {
+            t.loss = true;
             ind[(size_t)have2++] = ind[(size_t)i];
           } else {
-            imp.curr_tol = imp.curr_tol - (3.0 / 2.0) * diff;
-            while (imp.curr_tol < 0.0) imp.curr_tol += (1.0 / 10.0) * diff;
+            t.curr_tol = t.curr_tol - (3.0 / 2.0) * diff;
+            while (t.curr_tol < 0.0) t.curr_tol += (1.0 / 10.0) * diff;
           }
         }
       }
       have = have2;
     }
-    imp.passed = have >= imp.cur_num_rhs;
-    return imp.passed;
+    t.passed = have >= t.cur_num_rhs;
+    return t.passed;
+  }
+
+  bool conv_check(Iter &it) {  // StatusTestCombo SEQ (BelosStatusTestCombo.hpp:360-380)
+    if (!seq) return conv_passed = res_check(imp, it);
+    if (!res_check(imp, it)) return conv_passed = false;
+    return conv_passed = res_check(exp, it);
   }
 
   bool check(Iter &it) {  // StatusTestCombo OR: both members evaluated
@@ -875,7 +1007,7 @@ struct Engine {
       ~T() { S->t_check += since(t0); }
     } tm{S, t0};
     const bool a = max_iters_check(it);
-    const bool b = imp_check(it);
+    const bool b = conv_check(it);
     S->history.insert(S->history.end(), imp.testvector.begin(), imp.testvector.end());
     S->hist_cols = (int)imp.testvector.size();
     return a || b;
@@ -974,13 +1106,31 @@ struct Engine {
       const int lcl = it.cur_dim + k, c = it.cur_dim;
       MvPtr Vnext = view(*it.V, lcl, k);
       MvPtr Vprev = view(*it.V, c, k);
-      lp.apply(*Vprev, *Vnext);
+      MvPtr Znext;
+      if (it.Z.p) {  // BlockFGmresIter::iterate (BelosBlockFGmresIter.hpp:680-691)
+        Znext = view(*it.Z, c, k);
+        lp.apply_right_prec(*Vprev, *Znext);
+        lp.op(*Znext, *Vnext);
+      } else {
+        lp.apply(*Vprev, *Vnext);
+      }
       MvPtr Q = view(*it.V, 0, lcl);
       subH.assign((size_t)lcl * k, 0.0);
       subH2.assign((size_t)k * k, 0.0);
       auto t0 = Clock::now();
-      // X = A V_prev again, bit for bit, if the device ICGS has to restart from its input
-      const std::function<void()> regen = [&] { crs_apply(*lp.A, *Vprev, *Vnext, 1.0, 0.0); };
+      // X = Op V_prev again, bit for bit, if the device ICGS has to restart from its input
+      const std::function<void()> regen = [&] {
+        if (Znext.p)
+          crs_apply(*lp.A, *Znext, *Vnext, 1.0, 0.0);
+        else if (!lp.LP && !lp.RP)
+          crs_apply(*lp.A, *Vprev, *Vnext, 1.0, 0.0);
+        else {  // not counted: the reference copies its input instead
+          const long long na = S->n_apply, np = S->n_prec;
+          lp.apply(*Vprev, *Vnext);
+          S->n_apply = na;
+          S->n_prec = np;
+        }
+      };
       const int rank = S->use_fast && S->fast.supports(k)
                            ? S->fast.project_and_normalize(*Vnext, *Q, subH.data(), lcl, subH2.data(), k, &regen)
                            : S->ortho.project_and_normalize(*Vnext, *Q, subH.data(), lcl, subH2.data(), k);
@@ -995,7 +1145,7 @@ struct Engine {
     }
   }
 
-  // BlockGmresSolMgr::solve (BelosBlockGmresSolMgr.hpp:916-1303), non-flexible.
+  // BlockGmresSolMgr::solve (BelosBlockGmresSolMgr.hpp:916-1303), plain and flexible.
   bool solve() {
     const Params &p = S->p;
     int block = p.block_size;
@@ -1027,16 +1177,24 @@ struct Engine {
       it.nb = nb;
       it.sd = block * (nb + 1);
       it.V = MvPtr(mv_create(lp.X->ctx, lp.X->n_global, lp.X->n_local, it.sd));
+      if (flexible) it.Z = MvPtr(mv_create(lp.X->ctx, lp.X->n_global, lp.X->n_local, it.sd));
       it.R.assign((size_t)it.sd * (it.sd - block), 0.0);
       it.z.assign((size_t)it.sd * block, 0.0);
       it.beta.assign((size_t)it.sd, 0.0);
       it.cs.assign((size_t)it.sd, 0.0);
       it.sn.assign((size_t)it.sd, 0.0);
       MvPtr V0(mv_create(lp.X->ctx, lp.X->n_global, lp.X->n_local, block));
-      if (idx.back() == -1)
-        lp.curr_res_vec(*V0);
-      else {
-        MvPtr r0v(mv_view(lp.R0.p, idx.data(), (int)idx.size()));
+      // the first block: (preconditioned) residual, R0 for flexible GMRES (:1025-1047)
+      auto residual = [&](migmres_mv &R) {
+        if (flexible)
+          lp.curr_res_vec(R);
+        else
+          lp.curr_prec_res_vec(R);
+      };
+      if (idx.back() == -1) {
+        residual(*V0);
+      } else {
+        MvPtr r0v(mv_view(flexible ? lp.R0.p : &lp.pr0(), idx.data(), (int)idx.size()));
         mv_assign(*r0v, *V0);
       }
       std::vector<double> z0((size_t)block * block, 0.0);
@@ -1054,8 +1212,8 @@ struct Engine {
       while (true) {
         try {
           iterate(it);
-          if (imp.passed) {
-            if (imp.loss) {
+          if (conv_passed) {
+            if (exp_conv().loss) {
               S->loa = true;
               converged = false;
             }
@@ -1071,8 +1229,12 @@ struct Engine {
             ++restarts;
             auto tr0 = Clock::now();
             MvPtr upd = current_update(it);
-            if (upd.p) mv_add_mv(1.0, *lp.curX, 1.0, *upd, *lp.curX);
-            lp.curr_res_vec(*V0);
+            if (flexible) {  // the update is already preconditioned (:1114-1118)
+              if (upd.p) mv_add_mv(1.0, *lp.curX, 1.0, *upd, *lp.curX);
+            } else {
+              lp.update_solution(upd);
+            }
+            residual(*V0);
             std::fill(z0.begin(), z0.end(), 0.0);
             if (normalize(*V0, z0.data(), block) != block)
               throw Error(MIGMRES_ESTATE, "BlockGmresSolMgr: failed to compute initial block after restart");
@@ -1083,20 +1245,25 @@ struct Engine {
           }
         } catch (const OrthoFailure &) {
           if (block != 1) {
-            if (!imp.passed) converged = false;
+            if (!conv_passed) converged = false;
             break;
           }
           update_lsqr(it, it.cur_dim);
           check(it);
-          if (!imp.passed) converged = false;
+          if (!conv_passed) converged = false;
           break;
         }
       }
-      if (imp.have_soln) {
-        mv_add_mv(0.0, *imp.cur_soln, 1.0, *imp.cur_soln, *lp.curX);
-      } else {
+      // the solution of this block (:1190-1212)
+      if (flexible) {
         MvPtr upd = current_update(it);
         if (upd.p) mv_add_mv(1.0, *lp.curX, 1.0, *upd, *lp.curX);
+      } else if (exp_conv().have_soln) {
+        ResTest &e = exp_conv();
+        mv_add_mv(0.0, *e.cur_soln, 1.0, *e.cur_soln, *lp.curX);
+      } else {
+        MvPtr upd = current_update(it);
+        lp.update_solution(upd);
       }
       lp.set_curr_ls();
       S->n_restarts += restarts;
@@ -1110,7 +1277,10 @@ struct Engine {
     }
     MIG_HIP(hipStreamSynchronize(lp.X->ctx->stream));
     S->num_iters = mi_n_iters;
-    S->achieved_tol = imp.testvector.empty() ? 0.0 : *std::max_element(imp.testvector.begin(), imp.testvector.end());
+    // achievedTol (:1268-1290): the explicit test's values when it ran, else the implicit ones
+    const std::vector<double> *tv = &imp.testvector;
+    if (seq && !exp.testvector.empty()) tv = &exp.testvector;
+    S->achieved_tol = tv->empty() ? 0.0 : *std::max_element(tv->begin(), tv->end());
     return converged && !S->loa;
   }
 };
@@ -1146,6 +1316,10 @@ extern "C" int migmres_solver_set_int(migmres_solver *s, const char *name, long 
       s->p.max_restarts = (int)v;
     } else if (n == "Adaptive Block Size") {
       s->p.adaptive = v != 0;
+    } else if (n == "Flexible Gmres") {
+      s->p.flexible = v != 0;
+    } else if (n == "Explicit Residual Test") {
+      s->p.exp_res_test = v != 0;
     } else if (n == "Verbosity") {
       s->p.verbosity = (int)v;
     } else if (n == "Output Frequency") {
@@ -1174,8 +1348,12 @@ extern "C" int migmres_solver_set_string(migmres_solver *s, const char *name, co
                 "\"Orthogonalization\" must be either \"DGKS\", \"ICGS\", or \"IMGS\"");
       MIG_CHECK(val == "ICGS" || val == "DGKS", "\"IMGS\" is not implemented on the device path");
       s->p.ortho = val;
-    } else if (n == "Implicit Residual Scaling") {
-      MIG_CHECK(val == "Norm of Preconditioned Initial Residual", "only the default implicit scaling is supported");
+    } else if (n == "Implicit Residual Scaling" || n == "Explicit Residual Scaling") {
+      // convertStringToScaleType (BelosTypes.cpp:106-123); "User Provided" needs a user norm
+      MIG_CHECK(val == "Norm of Initial Residual" || val == "Norm of Preconditioned Initial Residual" ||
+                    val == "Norm of RHS" || val == "None",
+                "invalid residual scaling type \"" + val + "\"");
+      (n[0] == 'I' ? s->p.imp_scale : s->p.exp_scale) = val;
     } else {
       throw Error(MIGMRES_EINVAL, "unknown string parameter \"" + n + "\"");
     }
@@ -1190,7 +1368,7 @@ extern "C" int migmres_solver_solve(migmres_solver *s, migmres_crs *A, migmres_m
     MIG_CHECK(X->ncols == B->ncols && X->n_local == A->n_local && B->n_local == A->n_local,
               "LinearProblem: inconsistent X/B/A shapes");
     s->history.clear();
-    s->n_apply = s->n_explicit = s->n_restarts = s->n_block_iters = 0;
+    s->n_apply = s->n_explicit = s->n_restarts = s->n_block_iters = s->n_prec = 0;
     s->t_spmm = s->t_ortho = s->t_lsq = s->t_check = s->t_restart = s->t_setup = 0.0;
     const double comm0 = s->ctx->comm_seconds;
     auto t0 = Clock::now();
@@ -1199,11 +1377,24 @@ extern "C" int migmres_solver_solve(migmres_solver *s, migmres_crs *A, migmres_m
     E.lp.A = A;
     E.lp.X = X;
     E.lp.B = const_cast<migmres_mv *>(B);
+    E.lp.LP = s->left;
+    E.lp.RP = s->right;
+    for (migmres_prec *M : {s->left, s->right})
+      MIG_CHECK(!M || M->A->n_local == A->n_local, "preconditioner and operator row maps differ");
+    E.setup_status_tests(s->left != nullptr, s->right != nullptr);
     E.lp.set_problem();
     const bool ok = E.solve();
     s->t_total = since(t0);
     s->t_comm = s->ctx->comm_seconds - comm0;
     if (converged) *converged = ok ? 1 : 0;
+  });
+}
+
+extern "C" int migmres_solver_set_prec(migmres_solver *s, int side, migmres_prec *M) {
+  return guard([&] {
+    MIG_CHECK(s, "set_prec: null solver");
+    MIG_CHECK(side == MIGMRES_LEFT_PREC || side == MIGMRES_RIGHT_PREC, "set_prec: side must be left (0) or right (1)");
+    (side == MIGMRES_LEFT_PREC ? s->left : s->right) = M;
   });
 }
 
@@ -1226,8 +1417,9 @@ extern "C" int migmres_solver_history(const migmres_solver *s, double *out, int 
 }
 extern "C" int migmres_solver_counters(const migmres_solver *s, long long *out, int n) {
   return guard([&] {
-    const long long v[5] = {s->n_apply, s->n_explicit, s->n_restarts, s->ortho.sing_count, s->n_block_iters};
-    for (int i = 0; i < n && i < 5; ++i) out[i] = v[i];
+    const long long v[6] = {s->n_apply, s->n_explicit, s->n_restarts, s->ortho.sing_count, s->n_block_iters,
+                            s->n_prec};
+    for (int i = 0; i < n && i < 6; ++i) out[i] = v[i];
   });
 }
 extern "C" int migmres_solver_timers(const migmres_solver *s, double *out, int n) {

@@ -112,7 +112,7 @@ class CrsMatrix:
         generated natively on each rank."""
         h = C.c_void_p()
         call("migmres_crs_create_galeri", comm.h, kind.encode(), nx, ny, nz, C.byref(h))
-        n = nx * ny * (nz if kind == "Laplace3D" else 1)
+        n = nx * ny * (nz if kind in ("Laplace3D", "Brick3D") else 1)
         return cls(comm, n, _handle=h)
 
     def colmap(self):
