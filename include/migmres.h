@@ -198,14 +198,18 @@ int migmres_prec_diagonal(const migmres_prec *M, double *dinv_out);
 
 /* ---------------- solver manager (Belos::BlockGmresSolMgr) ---------------- */
 
-int migmres_solver_create(migmres_ctx *ctx, migmres_solver **out);
+int migmres_solver_create(migmres_ctx *ctx, migmres_solver **out);  /* "BLOCK GMRES" */
+/* Belos::SolverFactory::create by name (Belos_Details_EBelosSolverType.cpp:55-100): "GMRES",
+ * "PSEUDOBLOCK GMRES" (PseudoBlockGmresSolMgr, BelosPseudoBlockGmresSolMgr.hpp), "BLOCK GMRES",
+ * "FLEXIBLE GMRES" (BlockGmresSolMgr with "Flexible Gmres" = true). */
+int migmres_solver_create_named(migmres_ctx *ctx, const char *name, migmres_solver **out);
 int migmres_solver_destroy(migmres_solver *s);
 /* Belos ParameterList names (BelosBlockGmresSolMgr.hpp:438-486): "Block Size", "Num Blocks",
  * "Maximum Iterations", "Maximum Restarts", "Convergence Tolerance", "Adaptive Block Size",
  * "Flexible Gmres", "Explicit Residual Test", "Orthogonalization" ("ICGS" | "DGKS"),
  * "Implicit Residual Scaling", "Explicit Residual Scaling" ("Norm of Initial Residual" |
  * "Norm of Preconditioned Initial Residual" | "Norm of RHS" | "None"), "Verbosity",
- * "Output Frequency". */
+ * "Output Frequency"; pseudo-block only: "Deflation Quorum" (no "Flexible Gmres"). */
 int migmres_solver_set_int(migmres_solver *s, const char *name, long long value);
 int migmres_solver_set_double(migmres_solver *s, const char *name, double value);
 int migmres_solver_set_string(migmres_solver *s, const char *name, const char *value);
@@ -225,7 +229,8 @@ int migmres_solver_loa_detected(const migmres_solver *s, int *loa);
  * Returns the number of rows via *nrows; pass out == NULL to query. */
 int migmres_solver_history(const migmres_solver *s, double *out, int *nrows, int *ncols);
 /* Counters: [0] operator applies, [1] explicit residual checks, [2] restarts,
- * [3] blkOrthoSing fallbacks, [4] block iterations, [5] preconditioner applies. */
+ * [3] blkOrthoSing fallbacks, [4] block iterations, [5] preconditioner applies,
+ * [6] pseudo-block deflations. */
 int migmres_solver_counters(const migmres_solver *s, long long *out, int n);
 /* Seconds spent in named phases: [0] total solve, [1] SpMM, [2] orthogonalization,
  * [3] host least-squares, [4] communication, [5] status tests, [6] restarts, [7] setup.

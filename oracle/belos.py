@@ -344,13 +344,15 @@ class StatusTestImpResNorm:
     """StatusTestImpResNorm with scaling 'Norm of Preconditioned Initial Residual'
     (BelosStatusTestImpResNorm.hpp:492-749, 808-845)."""
 
-    def __init__(self, tol, scale_type="Norm of Preconditioned Initial Residual"):
+    def __init__(self, tol, scale_type="Norm of Preconditioned Initial Residual", quorum=-1):
         self.tol = tol
         self.scale_type = scale_type
+        self.quorum = quorum
         self.reset()
 
     def reset(self):
         self.status = None
+        self.ind = []
         self.curr_tol = self.tol
         self.first = True
         self.loss = False
@@ -425,7 +427,8 @@ class StatusTestImpResNorm:
                         while self.curr_tol < 0.0:
                             self.curr_tol += (1.0 / 10.0) * diff
             have = have2
-        need = self.cur_num_rhs
+        self.ind = ind[:have]
+        need = self.cur_num_rhs if self.quorum == -1 else self.quorum
         self.status = have >= need
         return self.status
 
@@ -436,14 +439,16 @@ class StatusTestGenResNorm:
 
     loss = False
 
-    def __init__(self, tol, explicit=False, scale_type="Norm of Preconditioned Initial Residual"):
+    def __init__(self, tol, explicit=False, scale_type="Norm of Preconditioned Initial Residual", quorum=-1):
         self.tol = tol
         self.explicit = explicit
         self.scale_type = scale_type
+        self.quorum = quorum
         self.reset()
 
     def reset(self):
         self.status = None
+        self.ind = []
         self.first = True
         self.cur_soln = None
         self.cur_ls_num = 0
@@ -482,7 +487,7 @@ class StatusTestGenResNorm:
             if p != -1:
                 s = 0.0 if self.scale is None else self.scale[p]
                 self.testvector[p] = self.resvector[p] / s / 1.0 if s != 0.0 else self.resvector[p] / 1.0
-        have = 0
+        self.ind = []
         for p in self.cur_idx:
             if p == -1:
                 continue
@@ -490,11 +495,12 @@ class StatusTestGenResNorm:
             if tv > self.tol:
                 pass
             elif tv <= self.tol:
-                have += 1
+                self.ind.append(p)
             else:
                 self.status = False
                 raise FloatingPointError("StatusTestGenResNorm: NaN detected")
-        self.status = have >= self.cur_num_rhs
+        need = self.cur_num_rhs if self.quorum == -1 else self.quorum
+        self.status = len(self.ind) >= need
         return self.status
 
 
@@ -515,6 +521,14 @@ class StatusTestSeq:
     @property
     def n_explicit(self):
         return sum(t.n_explicit for t in self.tests)
+
+    @property
+    def ind(self):
+        return self.tests[-1].ind
+
+    @property
+    def cur_soln(self):
+        return self.tests[-1].cur_soln
 
     def reset(self):
         for t in self.tests:

@@ -148,3 +148,42 @@ def test_explicit_residual_test_scalings(brick_problem, scale):
     den = {"Norm of RHS": np.linalg.norm(B, axis=0), "None": 1.0}.get(scale, np.linalg.norm(B, axis=0))
     tol = 1e-8 if scale != "None" else 1e-6
     assert (res / den).max() <= tol
+
+
+def test_pseudo_block_single_rhs_equals_block_gmres():
+    """PseudoBlockGmres with one right-hand side performs exactly BlockGmres(k = 1): same
+    single-vector ICGS, Givens LSQR and status tests."""
+    from oracle import pseudo
+    nx = 24
+    n = nx * nx
+    A = oe.DistCrs(lambda f, m: oe.laplace2d_rows(nx, nx, f, m), n, 1)
+    Xe, _ = oe.epetra_random_mv(9, n, 1)
+    B = A.apply(Xe)
+    P = {"Block Size": 1, "Num Blocks": 15, "Convergence Tolerance": 1e-9, "Orthogonalization": "ICGS",
+         "Maximum Restarts": 100}
+    r1 = pseudo.solve(A.apply, B, P)
+    r2 = ob.solve(A.apply, B, P)
+    assert r1["converged"] and r2["converged"]
+    assert r1["iterations"] == r2["iterations"] and r1["restarts"] == r2["restarts"]
+    np.testing.assert_array_equal(r1["history"], r2["history"])
+    np.testing.assert_array_equal(r1["X"], r2["X"])
+
+
+def test_pseudo_block_deflation():
+    """Right-hand sides converge at different steps and are deflated one by one; every
+    column ends below the tolerance."""
+    from oracle import pseudo
+    nx = 26
+    n = nx * nx
+    A = oe.DistCrs(lambda f, m: oe.laplace2d_rows(nx, nx, f, m), n, 1)
+    Xe, _ = oe.epetra_random_mv(3, n, 4)
+    Xe[:, 1] = np.sin(np.arange(n) * 0.01)          # smooth: converges fast
+    B = A.apply(Xe)
+    for q in (1, 2, 4):
+        r = pseudo.solve(A.apply, B, {"Block Size": 4, "Num Blocks": 20, "Convergence Tolerance": 1e-9,
+                                      "Deflation Quorum": q, "Maximum Restarts": 50})
+        assert r["converged"]
+        rel = np.linalg.norm(B - A.apply(r["X"]), axis=0) / np.linalg.norm(B, axis=0)
+        assert rel.max() <= 1e-9
+        if q == 1:
+            assert r["deflations"] >= 1

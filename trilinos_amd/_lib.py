@@ -75,6 +75,7 @@ _SIGS = {
     "migmres_prec_apply": [vp, vp, vp],
     "migmres_prec_diagonal": [vp, P(f64)],
     "migmres_solver_create": [vp, P(vp)],
+    "migmres_solver_create_named": [vp, C.c_char_p, P(vp)],
     "migmres_solver_set_prec": [vp, i32, vp],
     "migmres_solver_destroy": [vp],
     "migmres_solver_set_int": [vp, C.c_char_p, i64],

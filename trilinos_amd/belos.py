@@ -201,7 +201,7 @@ class LinearProblem:
 
 
 _INT_PARAMS = {"Block Size", "Num Blocks", "Maximum Iterations", "Maximum Restarts", "Verbosity",
-               "Output Frequency"}
+               "Output Frequency", "Deflation Quorum"}
 _BOOL_PARAMS = {"Adaptive Block Size", "Flexible Gmres", "Explicit Residual Test"}
 _DOUBLE_PARAMS = {"Convergence Tolerance"}
 _STRING_PARAMS = {"Orthogonalization", "Implicit Residual Scaling", "Explicit Residual Scaling"}
@@ -225,9 +225,12 @@ class BlockGmresSolMgr:
     default) orthogonalization run on the device path; "IMGS" raises at solve().
     """
 
+    _solver_name = "BLOCK GMRES"
+    _defaults = DEFAULT_PARAMETERS
+
     def __init__(self, problem=None, params=None):
         self.problem = problem
-        self.params = dict(DEFAULT_PARAMETERS)
+        self.params = dict(self._defaults)
         h = C.c_void_p()
         self.comm = None
         self.h = None
@@ -241,7 +244,7 @@ class BlockGmresSolMgr:
                 raise RuntimeError("BlockGmresSolMgr: no LinearProblem set")
             self.comm = self.problem.A.comm
             h = C.c_void_p()
-            call("migmres_solver_create", self.comm.h, C.byref(h))
+            call("migmres_solver_create_named", self.comm.h, self._solver_name.encode(), C.byref(h))
             self.h = h
             for k, v in self.params.items():
                 self._push(k, v)
@@ -265,12 +268,12 @@ class BlockGmresSolMgr:
         self.problem = problem
 
     def getValidParameters(self):
-        return dict(DEFAULT_PARAMETERS)
+        return dict(self._defaults)
 
     def setParameters(self, params):
         for k, v in params.items():
-            if k not in DEFAULT_PARAMETERS:
-                raise KeyError(f'"{k}" is not a valid BlockGmresSolMgr parameter')
+            if k not in self._defaults:
+                raise KeyError(f'"{k}" is not a valid {type(self).__name__} parameter')
             if k == "Block Size" and int(v) <= 0:
                 raise ValueError('"Block Size" must be strictly positive.')
             if k == "Num Blocks" and int(v) <= 0:
@@ -323,10 +326,10 @@ class BlockGmresSolMgr:
         return out[:nr.value * nc.value].reshape(nr.value, nc.value)
 
     def counters(self):
-        out = (C.c_longlong * 6)()
-        call("migmres_solver_counters", self.h, out, 6)
+        out = (C.c_longlong * 7)()
+        call("migmres_solver_counters", self.h, out, 7)
         keys = ("applies", "explicit_checks", "restarts", "blk_ortho_sing", "block_iterations",
-                "prec_applies")
+                "prec_applies", "deflations")
         return dict(zip(keys, list(out)))
 
     def timers(self):
@@ -341,3 +344,36 @@ class BlockGmresSolMgr:
                 call("migmres_solver_destroy", self.h)
         except Exception:
             pass
+
+
+# BelosPseudoBlockGmresSolMgr.hpp:494-507
+PSEUDO_DEFAULT_PARAMETERS = {
+    "Convergence Tolerance": 1e-8, "Maximum Restarts": 20, "Maximum Iterations": 1000,
+    "Num Blocks": 300, "Block Size": 1, "Verbosity": 0, "Output Frequency": -1,
+    "Deflation Quorum": 1, "Orthogonalization": "ICGS", "Explicit Residual Test": False,
+    "Implicit Residual Scaling": "Norm of Preconditioned Initial Residual",
+    "Explicit Residual Scaling": "Norm of Initial Residual",
+}
+
+
+class PseudoBlockGmresSolMgr(BlockGmresSolMgr):
+    """Belos::PseudoBlockGmresSolMgr over the device solver: "Block Size" single-vector
+    GMRES iterations sharing each operator application, with deflation of converged
+    right-hand sides ("Deflation Quorum")."""
+
+    _solver_name = "PSEUDOBLOCK GMRES"
+    _defaults = PSEUDO_DEFAULT_PARAMETERS
+
+
+def SolverFactory(name, problem=None, params=None):
+    """Belos::SolverFactory::create for the GMRES family (Belos_Details_EBelosSolverType.cpp)."""
+    n = name.upper()
+    if n in ("GMRES", "PSEUDOBLOCK GMRES", "PSEUDO BLOCK GMRES", "PSEUDOBLOCKGMRES"):
+        return PseudoBlockGmresSolMgr(problem, params)
+    if n == "BLOCK GMRES":
+        return BlockGmresSolMgr(problem, params)
+    if n == "FLEXIBLE GMRES":
+        p = dict(params or {})
+        p["Flexible Gmres"] = True
+        return BlockGmresSolMgr(problem, p)
+    raise ValueError(f'solver "{name}" is not implemented on the device path')

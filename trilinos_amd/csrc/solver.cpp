@@ -597,6 +597,8 @@ struct Params {
   bool adaptive = true;
   bool flexible = false;
   bool exp_res_test = false;
+  bool pseudo = false;  // PseudoBlockGmresSolMgr instead of BlockGmresSolMgr
+  int def_quorum = 1;   // "Deflation Quorum" (pseudo-block only)
   std::string ortho = "DGKS";
   std::string imp_scale = "Norm of Preconditioned Initial Residual";
   std::string exp_scale = "Norm of Initial Residual";
@@ -622,7 +624,7 @@ struct migmres_solver {
   bool loa = false;
   std::vector<double> history;
   int hist_cols = 0;
-  long long n_apply = 0, n_explicit = 0, n_restarts = 0, n_block_iters = 0, n_prec = 0;
+  long long n_apply = 0, n_explicit = 0, n_restarts = 0, n_block_iters = 0, n_prec = 0, n_deflations = 0;
   double t_total = 0, t_spmm = 0, t_ortho = 0, t_lsq = 0, t_comm = 0;
   double t_check = 0, t_restart = 0, t_setup = 0;
   bool sync_timers() const { return (p.verbosity & 1) != 0; }
@@ -799,6 +801,8 @@ struct ResTest {
   std::vector<double> scale, resvector, testvector;
   MvPtr cur_soln;
   bool have_soln = false;
+  int quorum = -1;       // setQuorum: passes when >= quorum columns pass (-1: all)
+  std::vector<int> ind;  // convIndices(): the right-hand sides that passed
   ResTest(Kind k, double t, const std::string &st) : kind(k), scale_type(st), tol(t), curr_tol(t) {}
 };
 
@@ -909,6 +913,12 @@ struct Engine {
   }
 
   bool res_check(ResTest &t, Iter &it) {
+    return res_check(t, [&] { return native_residuals(it); }, [&] { return current_update(it); });
+  }
+  // checkStatus of either test over any iteration: native residual norms and the current
+  // solution update come from the callbacks (BlockGmresIter or PseudoBlockGmresIter).
+  bool res_check(ResTest &t, const std::function<std::vector<double>()> &native,
+                 const std::function<MvPtr()> &update) {
     if (t.first) {
       t.first = false;
       scale_setup(t);
@@ -934,7 +944,7 @@ struct Engine {
     auto explicit_norms = [&](std::vector<double> &out) {
       ++t.n_explicit;
       ++S->n_explicit;
-      MvPtr upd = current_update(it);
+      MvPtr upd = update();
       if (!t.cur_soln.p || t.cur_soln->ncols != k) t.cur_soln = lp.clone(k);
       lp.updated_solution(upd, *t.cur_soln);
       t.have_soln = true;
@@ -947,7 +957,7 @@ struct Engine {
     if (t.kind == ResTest::GEN_EXPLICIT)
       explicit_norms(res);
     else
-      res = native_residuals(it);
+      res = native();
     for (size_t i = 0; i < t.cur_idx.size(); ++i)
       if (t.cur_idx[i] != -1) t.resvector[(size_t)t.cur_idx[i]] = res[i];
     for (int p : t.cur_idx)
@@ -989,7 +999,8 @@ struct Engine {
       }
       have = have2;
     }
-    t.passed = have >= t.cur_num_rhs;
+    t.ind.assign(ind.begin(), ind.begin() + have);
+    t.passed = have >= (t.quorum == -1 ? t.cur_num_rhs : t.quorum);
     return t.passed;
   }
 
@@ -1285,6 +1296,261 @@ struct Engine {
   }
 };
 
+// ------------------------------------------------------------------------------------
+// Pseudo-block GMRES: k single-vector GMRES iterations sharing one operator application per
+// step (BelosPseudoBlockGmresIter.hpp, BelosPseudoBlockGmresSolMgr.hpp).  Right-hand side i
+// owns the basis slot V[:, slot*(nb+1) .. slot*(nb+1)+nb] of one device multivector; its
+// Hessenberg column, Givens rotations and least-squares right-hand side stay on the host.
+// Deflation of converged right-hand sides drops their state; slots are never moved.
+// ------------------------------------------------------------------------------------
+struct PseudoRhs {
+  int slot;
+  std::vector<double> H, z, cs, sn;  // H is (nb+1) x nb column-major
+};
+
+struct PseudoIter {
+  int nb = 0, cur_dim = 0, num_iters = 0;
+  MvPtr V;  // N x nslots*(nb+1)
+  std::vector<PseudoRhs> st;
+  int col(const PseudoRhs &r, int j) const { return r.slot * (nb + 1) + j; }
+  double &Hat(PseudoRhs &r, int i, int j) const { return r.H[(size_t)i + (size_t)j * (nb + 1)]; }
+};
+
+struct PseudoEngine : Engine {
+  PseudoEngine(migmres_solver *s, double tol, int mi) : Engine(s, tol, mi) {}
+
+  void setup_pseudo_tests(bool has_left) {  // checkStatusTest (:1156-1265)
+    seq = S->p.exp_res_test || has_left;
+    imp.kind = seq ? ResTest::GEN_IMPLICIT : ResTest::IMP_RES_NORM;
+    imp.quorum = exp.quorum = S->p.def_quorum;
+  }
+
+  std::vector<double> native(PseudoIter &it) {  // getNativeResiduals (:487-510)
+    std::vector<double> r(it.st.size());
+    for (size_t i = 0; i < it.st.size(); ++i) r[i] = std::fabs(it.st[i].z[(size_t)it.cur_dim]);
+    return r;
+  }
+
+  MvPtr update(PseudoIter &it) {  // getCurrentUpdate (:447-484)
+    const int c = it.cur_dim;
+    if (c == 0) return MvPtr();
+    const int n = (int)it.st.size();
+    MvPtr upd = lp.clone(n);
+    std::vector<double> y((size_t)c);
+    for (int i = 0; i < n; ++i) {
+      PseudoRhs &r = it.st[(size_t)i];
+      for (int q = 0; q < c; ++q) y[(size_t)q] = r.z[(size_t)q];
+      for (int q = c - 1; q >= 0; --q) {
+        double t = y[(size_t)q];
+        for (int u = q + 1; u < c; ++u) t -= it.Hat(r, q, u) * y[(size_t)u];
+        y[(size_t)q] = t / it.Hat(r, q, q);
+      }
+      MvPtr Vi = view(*it.V, it.col(r, 0), c);
+      MvPtr ui = view(*upd, i, 1);
+      mv_times_mat_add_mv(1.0, *Vi, y.data(), c, 0.0, *ui);
+    }
+    return upd;
+  }
+
+  bool check(PseudoIter &it) {
+    auto t0 = Clock::now();
+    mi_n_iters = it.num_iters;
+    mi_passed = mi_n_iters >= max_iters;
+    auto nat = [&] { return native(it); };
+    auto upd = [&] { return update(it); };
+    if (!seq)
+      conv_passed = res_check(imp, nat, upd);
+    else
+      conv_passed = res_check(imp, nat, upd) && res_check(exp, nat, upd);
+    S->history.insert(S->history.end(), imp.testvector.begin(), imp.testvector.end());
+    S->hist_cols = (int)imp.testvector.size();
+    S->t_check += since(t0);
+    return mi_passed || conv_passed;
+  }
+
+  // iterate (BelosPseudoBlockGmresIter.hpp:743-871): AU = Op U, then each right-hand side
+  // projects and normalises its own new vector against its own basis.
+  void iterate(PseudoIter &it) {
+    const int n = (int)it.st.size();
+    std::vector<int> ucols((size_t)n), vcols((size_t)n);
+    std::vector<double> h, r(1);
+    while (!check(it) && it.cur_dim < it.nb) {
+      ++it.num_iters;
+      ++S->n_block_iters;
+      const int c = it.cur_dim;
+      for (int i = 0; i < n; ++i) {
+        ucols[(size_t)i] = it.col(it.st[(size_t)i], c);
+        vcols[(size_t)i] = it.col(it.st[(size_t)i], c + 1);
+      }
+      MvPtr U(mv_view(it.V.p, ucols.data(), n));
+      MvPtr AU(mv_view(it.V.p, vcols.data(), n));
+      lp.apply(*U, *AU);
+      auto t0 = Clock::now();
+      h.assign((size_t)c + 1, 0.0);
+      for (int i = 0; i < n; ++i) {
+        PseudoRhs &rs = it.st[(size_t)i];
+        MvPtr w = view(*it.V, vcols[(size_t)i], 1);
+        MvPtr Q = view(*it.V, it.col(rs, 0), c + 1);
+        S->ortho.project_and_normalize(*w, *Q, h.data(), c + 1, r.data(), 1);
+        for (int q = 0; q <= c; ++q) it.Hat(rs, q, c) = h[(size_t)q];
+        it.Hat(rs, c + 1, c) = r[0];
+      }
+      S->t_ortho += since(t0);
+      update_lsqr(it);
+      it.cur_dim += 1;
+    }
+  }
+
+  void update_lsqr(PseudoIter &it) {  // updateLSQR (:876-915), Givens per right-hand side
+    const int c = it.cur_dim;
+    for (PseudoRhs &r : it.st) {
+      for (int j = 0; j < c; ++j) {
+        const double x = it.Hat(r, j, c), y = it.Hat(r, j + 1, c);
+        it.Hat(r, j, c) = r.cs[(size_t)j] * x + r.sn[(size_t)j] * y;
+        it.Hat(r, j + 1, c) = r.cs[(size_t)j] * y - r.sn[(size_t)j] * x;
+      }
+      rotg(it.Hat(r, c, c), it.Hat(r, c + 1, c), r.cs[(size_t)c], r.sn[(size_t)c]);
+      it.Hat(r, c + 1, c) = 0.0;
+      const double x = r.z[(size_t)c], y = r.z[(size_t)c + 1];
+      r.z[(size_t)c] = r.cs[(size_t)c] * x + r.sn[(size_t)c] * y;
+      r.z[(size_t)c + 1] = r.cs[(size_t)c] * y - r.sn[(size_t)c] * x;
+    }
+  }
+
+  // Fresh states: R's columns normalised one by one into slot column 0 (:1340-1360).
+  void start_states(PseudoIter &it, migmres_mv &R) {
+    const int n = R.ncols;
+    it.st.assign((size_t)n, PseudoRhs());
+    for (int i = 0; i < n; ++i) {
+      PseudoRhs &r = it.st[(size_t)i];
+      r.slot = i;
+      r.H.assign((size_t)(it.nb + 1) * it.nb, 0.0);
+      r.z.assign((size_t)it.nb + 1, 0.0);
+      r.cs.assign((size_t)it.nb + 1, 0.0);
+      r.sn.assign((size_t)it.nb + 1, 0.0);
+      MvPtr src = view(R, i, 1);
+      MvPtr v0 = view(*it.V, it.col(r, 0), 1);
+      mv_assign(*src, *v0);
+      double b = 0.0;
+      if (S->ortho.normalize(*v0, &b, 1) != 1)
+        throw Error(MIGMRES_ESTATE, "PseudoBlockGmresSolMgr: failed to compute initial block of orthonormal vectors");
+      r.z[0] = b;
+    }
+    it.cur_dim = 0;
+  }
+
+  // PseudoBlockGmresSolMgr::solve (BelosPseudoBlockGmresSolMgr.hpp:1268-1668)
+  bool solve() {
+    const Params &p = S->p;
+    int block = p.block_size;
+    const int numrhs = lp.B->ncols;
+    int start = 0, to_solve = numrhs;
+    int cur = std::min(to_solve, block);
+    block = cur;
+    std::vector<int> idx;
+    for (int i = 0; i < cur; ++i) idx.push_back(start + i);
+    lp.set_ls_index(idx);
+    bool converged = true;
+    S->loa = false;
+    S->ortho.dgks = p.ortho == "DGKS";
+    PseudoIter it;
+    it.nb = p.num_blocks;
+    it.V = MvPtr(mv_create(lp.X->ctx, lp.X->n_global, lp.X->n_local, block * (p.num_blocks + 1)));
+    while (to_solve > 0) {
+      auto ts0 = Clock::now();
+      std::vector<int> cur_idx(idx.begin(), idx.begin() + cur);
+      it.num_iters = 0;
+      {
+        MvPtr R0(mv_view(&lp.pr0(), idx.data(), (int)idx.size()));
+        start_states(it, *R0);
+      }
+      S->t_setup += since(ts0);
+      int restarts = 0;
+      while (true) {
+        iterate(it);
+        if (conv_passed) {
+          if (exp_conv().loss) {
+            S->loa = true;
+            converged = false;
+          }
+          const std::vector<int> conv_idx = exp_conv().ind;
+          if (conv_idx.size() == cur_idx.size()) break;
+          // deflate the converged right-hand sides (:1397-1466)
+          lp.set_curr_ls();
+          std::vector<int> keep, def;
+          for (size_t i = 0; i < cur_idx.size(); ++i) {
+            const bool found = std::find(conv_idx.begin(), conv_idx.end(), cur_idx[i]) != conv_idx.end();
+            (found ? def : keep).push_back((int)i);
+          }
+          if (it.cur_dim) {
+            MvPtr upd = update(it);
+            MvPtr dupd(mv_view(upd.p, def.data(), (int)def.size()));
+            lp.set_ls_index(conv_idx);
+            if (lp.RP) {
+              MvPtr ru = lp.clone(dupd->ncols);
+              lp.prec(*lp.RP, *dupd, *ru);
+              mv_add_mv(1.0, *lp.curX, 1.0, *ru, *lp.curX);
+            } else {
+              mv_add_mv(1.0, *lp.curX, 1.0, *dupd, *lp.curX);
+            }
+          }
+          std::vector<int> kept_idx;
+          std::vector<PseudoRhs> kept;
+          for (int i : keep) {
+            kept_idx.push_back(cur_idx[(size_t)i]);
+            kept.push_back(std::move(it.st[(size_t)i]));
+          }
+          cur_idx = kept_idx;
+          lp.set_ls_index(cur_idx);
+          it.st = std::move(kept);
+          ++S->n_deflations;
+        } else if (mi_passed) {
+          converged = false;
+          break;
+        } else if (it.cur_dim == it.nb) {
+          if (restarts >= p.max_restarts) {
+            converged = false;
+            break;
+          }
+          ++restarts;
+          auto tr0 = Clock::now();
+          lp.update_solution(update(it));
+          MvPtr R0 = lp.clone((int)cur_idx.size());
+          lp.curr_prec_res_vec(*R0);
+          start_states(it, *R0);
+          S->t_restart += since(tr0);
+        } else {
+          throw Error(MIGMRES_ESTATE, "PseudoBlockGmresSolMgr: invalid return from iterate()");
+        }
+      }
+      if (exp_conv().have_soln) {
+        ResTest &e = exp_conv();
+        mv_add_mv(0.0, *e.cur_soln, 1.0, *e.cur_soln, *lp.curX);
+      } else {
+        lp.update_solution(update(it));
+      }
+      lp.set_curr_ls();
+      S->n_restarts += restarts;
+      start += cur;
+      to_solve -= cur;
+      if (to_solve > 0) {
+        cur = std::min(to_solve, block);
+        block = cur;
+        idx.clear();
+        for (int i = 0; i < cur; ++i) idx.push_back(start + i);
+        if (p.def_quorum > block) imp.quorum = exp.quorum = block;
+        lp.set_ls_index(idx);
+      }
+    }
+    MIG_HIP(hipStreamSynchronize(lp.X->ctx->stream));
+    S->num_iters = mi_n_iters;
+    const std::vector<double> *tv = &imp.testvector;
+    if (seq && !exp.testvector.empty()) tv = &exp.testvector;
+    S->achieved_tol = tv->empty() ? 0.0 : *std::max_element(tv->begin(), tv->end());
+    return converged && !S->loa;
+  }
+};
+
 }  // namespace
 
 
@@ -1293,6 +1559,30 @@ extern "C" int migmres_solver_create(migmres_ctx *ctx, migmres_solver **out) {
     MIG_CHECK(ctx && out, "bad solver arguments");
     auto *s = new migmres_solver();
     s->ctx = ctx;
+    *out = s;
+  });
+}
+
+// SolverFactory names (Belos_Details_EBelosSolverType.cpp:55-100, reviseParameterListForAlias
+// :213-222): "GMRES" / "PSEUDOBLOCK GMRES" -> PseudoBlockGmresSolMgr, "BLOCK GMRES" ->
+// BlockGmresSolMgr, "FLEXIBLE GMRES" -> BlockGmresSolMgr with "Flexible Gmres" = true.
+extern "C" int migmres_solver_create_named(migmres_ctx *ctx, const char *name, migmres_solver **out) {
+  return guard([&] {
+    MIG_CHECK(ctx && out && name, "bad solver arguments");
+    std::string n(name);
+    for (char &ch : n) ch = (char)std::toupper((unsigned char)ch);
+    bool pseudo = false, flexible = false;
+    if (n == "GMRES" || n == "PSEUDOBLOCK GMRES" || n == "PSEUDO BLOCK GMRES" || n == "PSEUDOBLOCKGMRES")
+      pseudo = true;
+    else if (n == "FLEXIBLE GMRES")
+      flexible = true;
+    else if (n != "BLOCK GMRES")
+      throw Error(MIGMRES_EINVAL, "solver \"" + std::string(name) + "\" is not implemented on the device path");
+    auto *s = new migmres_solver();
+    s->ctx = ctx;
+    s->p.pseudo = pseudo;
+    s->p.flexible = flexible;
+    if (pseudo) s->p.ortho = "ICGS";  // BelosPseudoBlockGmresSolMgr.hpp:506
     *out = s;
   });
 }
@@ -1317,7 +1607,12 @@ extern "C" int migmres_solver_set_int(migmres_solver *s, const char *name, long 
     } else if (n == "Adaptive Block Size") {
       s->p.adaptive = v != 0;
     } else if (n == "Flexible Gmres") {
+      MIG_CHECK(!s->p.pseudo, "\"Flexible Gmres\" is not a PseudoBlockGmresSolMgr parameter");
       s->p.flexible = v != 0;
+    } else if (n == "Deflation Quorum") {
+      MIG_CHECK(s->p.pseudo, "\"Deflation Quorum\" is a PseudoBlockGmresSolMgr parameter");
+      MIG_CHECK(v >= 1, "\"Deflation Quorum\" must be positive");
+      s->p.def_quorum = (int)v;
     } else if (n == "Explicit Residual Test") {
       s->p.exp_res_test = v != 0;
     } else if (n == "Verbosity") {
@@ -1368,22 +1663,38 @@ extern "C" int migmres_solver_solve(migmres_solver *s, migmres_crs *A, migmres_m
     MIG_CHECK(X->ncols == B->ncols && X->n_local == A->n_local && B->n_local == A->n_local,
               "LinearProblem: inconsistent X/B/A shapes");
     s->history.clear();
-    s->n_apply = s->n_explicit = s->n_restarts = s->n_block_iters = s->n_prec = 0;
+    s->n_apply = s->n_explicit = s->n_restarts = s->n_block_iters = s->n_prec = s->n_deflations = 0;
     s->t_spmm = s->t_ortho = s->t_lsq = s->t_check = s->t_restart = s->t_setup = 0.0;
     const double comm0 = s->ctx->comm_seconds;
     auto t0 = Clock::now();
-    Engine E(s, s->p.tol, s->p.max_iters);
-    E.lp.S = s;
-    E.lp.A = A;
-    E.lp.X = X;
-    E.lp.B = const_cast<migmres_mv *>(B);
-    E.lp.LP = s->left;
-    E.lp.RP = s->right;
     for (migmres_prec *M : {s->left, s->right})
       MIG_CHECK(!M || M->A->n_local == A->n_local, "preconditioner and operator row maps differ");
-    E.setup_status_tests(s->left != nullptr, s->right != nullptr);
-    E.lp.set_problem();
-    const bool ok = E.solve();
+    bool ok;
+    if (s->p.pseudo) {
+      MIG_CHECK(s->p.def_quorum <= s->p.block_size,
+                "\"Deflation Quorum\" must not be larger than \"Block Size\" (BelosPseudoBlockGmresSolMgr.hpp:994-999)");
+      PseudoEngine E(s, s->p.tol, s->p.max_iters);
+      E.lp.S = s;
+      E.lp.A = A;
+      E.lp.X = X;
+      E.lp.B = const_cast<migmres_mv *>(B);
+      E.lp.LP = s->left;
+      E.lp.RP = s->right;
+      E.setup_pseudo_tests(s->left != nullptr);
+      E.lp.set_problem();
+      ok = E.solve();
+    } else {
+      Engine E(s, s->p.tol, s->p.max_iters);
+      E.lp.S = s;
+      E.lp.A = A;
+      E.lp.X = X;
+      E.lp.B = const_cast<migmres_mv *>(B);
+      E.lp.LP = s->left;
+      E.lp.RP = s->right;
+      E.setup_status_tests(s->left != nullptr, s->right != nullptr);
+      E.lp.set_problem();
+      ok = E.solve();
+    }
     s->t_total = since(t0);
     s->t_comm = s->ctx->comm_seconds - comm0;
     if (converged) *converged = ok ? 1 : 0;
@@ -1417,9 +1728,9 @@ extern "C" int migmres_solver_history(const migmres_solver *s, double *out, int 
 }
 extern "C" int migmres_solver_counters(const migmres_solver *s, long long *out, int n) {
   return guard([&] {
-    const long long v[6] = {s->n_apply, s->n_explicit, s->n_restarts, s->ortho.sing_count, s->n_block_iters,
-                            s->n_prec};
-    for (int i = 0; i < n && i < 6; ++i) out[i] = v[i];
+    const long long v[7] = {s->n_apply, s->n_explicit, s->n_restarts, s->ortho.sing_count, s->n_block_iters,
+                            s->n_prec, s->n_deflations};
+    for (int i = 0; i < n && i < 7; ++i) out[i] = v[i];
   });
 }
 extern "C" int migmres_solver_timers(const migmres_solver *s, double *out, int n) {
