@@ -53,16 +53,20 @@ def test_spmm_bit_exact(comm, kind, dims, k):
 
 
 @pytest.mark.parametrize("per_row,k,pairs", [(4, 8, "default"), (5, 3, "default"), (12, 8, "default"),
-                                              (7, 8, "off")])
+                                              (7, 8, "off"), (30, 5, "default"), (75, 4, "default"),
+                                              (9, 8, "csr"), (0, 2, "default")])
 def test_spmm_unstructured_bit_exact(comm, per_row, k, pairs, monkeypatch):
-    """Unstructured rows through both SpMM kernels: the row-pair kernel (rows of <= 8
-    entries whose pairs need <= 12 keys) and the row-per-thread kernel (longer rows, or the
-    pair plan switched off with MIGMRES_NO_PAIR_SPMM=1)."""
+    """Unstructured rows through all three SpMM kernels: the row-pair kernel (rows of <= 8
+    entries whose pairs need <= 12 keys), the SELL-64 row kernel (longer rows, or the pair
+    plan switched off with MIGMRES_NO_PAIR_SPMM=1) and the plain CSR row kernel
+    (MIGMRES_NO_SELL_SPMM=1).  per_row 0: random row lengths 0..40 (empty rows included)."""
     import trilinos_amd as ta
     from oracle import epetra as oe
     from tests.test_plans import random_rows
-    if pairs == "off":
+    if pairs in ("off", "csr"):
         monkeypatch.setenv("MIGMRES_NO_PAIR_SPMM", "1")
+    if pairs == "csr":
+        monkeypatch.setenv("MIGMRES_NO_SELL_SPMM", "1")
     n = 3001
     rp, gc, vv = random_rows(n, 0, n, 29, per_row=per_row)
     A = ta.CrsMatrix(comm, n, rp, gc, vv)

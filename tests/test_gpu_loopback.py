@@ -56,6 +56,8 @@ def _gen(kind, dims):
         return nx * ny * nz, lambda f, m: oe.laplace3d_rows(nx, ny, nz, f, m)
     if kind == "Laplace2D":
         return nx * ny, lambda f, m: oe.laplace2d_rows(nx, ny, f, m)
+    if kind == "Brick3D":
+        return nx * ny * nz, lambda f, m: oe.brick3d_rows(nx, ny, nz, f, m)
     from tests.test_plans import random_rows
     n = nx
     return n, lambda f, m: random_rows(n, f, m, 41, per_row=ny)
@@ -63,7 +65,8 @@ def _gen(kind, dims):
 
 @pytest.mark.parametrize("kind,dims,k,P", [("Laplace3D", (16, 16, 16), 8, 2), ("Laplace2D", (37, 23, 1), 3, 3),
                                            ("Laplace3D", (9, 7, 5), 5, 4), ("random", (601, 4, 1), 8, 2),
-                                           ("random", (500, 11, 1), 2, 3)])
+                                           ("random", (500, 11, 1), 2, 3), ("Brick3D", (9, 8, 7), 8, 3),
+                                           ("random", (700, 0, 1), 4, 2)])
 def test_distributed_spmm_bit_exact(kind, dims, k, P):
     import trilinos_amd as ta
     from oracle import epetra as oe

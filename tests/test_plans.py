@@ -48,11 +48,16 @@ def lib_plan(n_global, P, p, rowptr, gcols, vals):
 
 def random_rows(n_global, first, nloc, seed, per_row=6):
     """Unstructured rows: random global columns in arbitrary insertion order, so remote
-    first-encounter order is NOT sorted by owner (exercises the non-stable shell sort)."""
+    first-encounter order is NOT sorted by owner (exercises the non-stable shell sort).
+    per_row = 0: random lengths 0..40, a length-0 row is empty (no diagonal either)."""
     rng = np.random.default_rng(seed + first)
     rows, cols, vals = [0], [], []
     for r in range(nloc):
-        c = rng.choice(n_global, size=per_row, replace=False)
+        m = per_row if per_row > 0 else int(rng.integers(0, 41))
+        if m == 0 and per_row == 0:
+            rows.append(len(cols))
+            continue
+        c = rng.choice(n_global, size=m, replace=False)
         c = np.concatenate([c[c != first + r], [first + r]])
         cols.extend(c.tolist())
         vals.extend(rng.standard_normal(len(c)).tolist())

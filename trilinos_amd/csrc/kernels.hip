@@ -129,6 +129,108 @@ void launch_spmm(hipStream_t s, int row_begin, int row_end, const int *rowptr, c
 }
 
 // -------------------------------------------------------------------------------------
+// SpMM x k for rows too long for the row-pair plan (27-point stencils, unstructured
+// matrices): one thread per row over a SELL-64 copy of the CSR (make_sell64), so each
+// column-index / value load of a wave is one contiguous 256 / 512-byte segment.  Sums in
+// stored order, products v * x, no FMA: bit-identical to k_spmm and the reference loop.
+// -------------------------------------------------------------------------------------
+template <int KC>
+__global__ __launch_bounds__(256) void k_spmm_sell(int n, const long long *__restrict__ off,
+                                                   const int *__restrict__ len, const int *__restrict__ scol,
+                                                   const double *__restrict__ sval, MvDesc X, int n_local,
+                                                   const double *__restrict__ ghost, long long ldg, MvDesc Y,
+                                                   int c0, int kc, double alpha, double beta,
+                                                   const int *__restrict__ sel, int nsel) {
+#pragma clang fp contract(off)
+  constexpr int J = KC >= 4 ? 4 : 8;  // entries whose KC x loads are issued together
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  int r;
+  if (sel) {
+    if (t >= nsel) return;
+    r = sel[t];
+  } else {
+    if (t >= n) return;
+    r = t;
+  }
+  const double *xc[KC];
+  const double *gc[KC];
+  double sum[KC];
+#pragma unroll
+  for (int c = 0; c < KC; ++c) {
+    sum[c] = 0.0;
+    xc[c] = colp(X, c0 + (c < kc ? c : 0));
+    gc[c] = ghost + (long long)(c0 + (c < kc ? c : 0)) * ldg;
+  }
+  const long long base = off[r >> 6] + (r & 63);
+  const int L = len[r];
+  for (int sb = 0; sb < L; sb += 8) {
+    int ci[8];
+    double v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const long long e = base + (long long)((sb + j < L) ? sb + j : L - 1) * 64;
+      ci[j] = scol[e];
+      v[j] = sval[e];
+    }
+    // J entries' gathers in flight before any is consumed: left to itself the compiler
+    // issues one load, waits, multiplies, and only then issues the next (latency-bound,
+    // 1.4x slower on the 27-point stencil, tools/mb_spmm27.hip)
+#pragma unroll
+    for (int j0 = 0; j0 < 8; j0 += J) {
+      double xv[J][KC];
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        const int col = ci[j0 + j];
+        const bool own = col < n_local;
+#pragma unroll
+        for (int c = 0; c < KC; ++c) xv[j][c] = *(own ? xc[c] + col : gc[c] + (col - n_local));
+      }
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        const bool ok = sb + j0 + j < L;
+#pragma unroll
+        for (int c = 0; c < KC; ++c) {
+          const double prod = v[j0 + j] * xv[j][c];
+          sum[c] = sum[c] + (ok ? prod : 0.0);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < KC; ++c) {
+    if (c < kc) {
+      double *yp = colp(Y, c0 + c) + r;
+      if (beta == 0.0)
+        *yp = (alpha == 1.0) ? sum[c] : alpha * sum[c];
+      else
+        *yp = alpha * sum[c] + beta * (*yp);
+    }
+  }
+}
+
+void launch_spmm_sell(hipStream_t s, int n_local, const long long *off, const int *len, const int *scol,
+                      const double *sval, MvDesc X, const double *ghost, long long ldg, MvDesc Y, double alpha,
+                      double beta, const int *sel, int nsel) {
+  const int n = sel ? nsel : n_local;
+  if (n <= 0) return;
+  const int k = Y.ncols;
+  const dim3 grid(cdiv(n, 256));
+  for (int c0 = 0; c0 < k; c0 += 8) {
+    const int kc = (k - c0) < 8 ? (k - c0) : 8;
+    if (kc == 1)
+      k_spmm_sell<1><<<grid, 256, 0, s>>>(n_local, off, len, scol, sval, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel);
+    else if (kc <= 2)
+      k_spmm_sell<2><<<grid, 256, 0, s>>>(n_local, off, len, scol, sval, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel);
+    else if (kc <= 4)
+      k_spmm_sell<4><<<grid, 256, 0, s>>>(n_local, off, len, scol, sval, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel);
+    else
+      k_spmm_sell<8><<<grid, 256, 0, s>>>(n_local, off, len, scol, sval, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel);
+    LAUNCH_CHECK();
+  }
+}
+
+// -------------------------------------------------------------------------------------
 // SpMM x k over row pairs (plan: make_pair_plan, plan.cpp).  One thread per row pair; every
 // X read is a 16-byte load of an aligned pair of rows shared by both rows of the pair (the
 // 8-byte gathers of k_spmm were instruction-bound: tools/mb_spmm.hip measured 1.35 ms

@@ -298,4 +298,35 @@ void make_pair_sell(int n_local, const long long *rowptr, const double *lvals, c
   }
 }
 
+void make_sell64(int n_local, const long long *rowptr, const int *lcols, const double *lvals, Sell64 &out) {
+  const int nchunks = (n_local + 63) / 64;
+  out.off.assign((size_t)nchunks + 1, 0);
+  out.len.assign((size_t)n_local, 0);
+  for (int c = 0; c < nchunks; ++c) {
+    int w = 0;
+    for (int r = 64 * c; r < std::min(n_local, 64 * c + 64); ++r) {
+      out.len[(size_t)r] = (int)(rowptr[r + 1] - rowptr[r]);
+      w = std::max(w, out.len[(size_t)r]);
+    }
+    out.off[(size_t)c + 1] = out.off[(size_t)c] + (long long)w * 64;
+  }
+  out.cols.assign((size_t)out.off[(size_t)nchunks], 0);
+  out.vals.assign((size_t)out.off[(size_t)nchunks], 0.0);
+  for (int c = 0; c < nchunks; ++c) {
+    const int w = (int)((out.off[(size_t)c + 1] - out.off[(size_t)c]) / 64);
+    for (int lane = 0; lane < 64; ++lane) {
+      const int r = 64 * c + lane;
+      for (int s = 0; s < w; ++s) {
+        const size_t at = (size_t)out.off[(size_t)c] + (size_t)s * 64 + lane;
+        if (r < n_local && s < out.len[(size_t)r]) {
+          out.cols[at] = lcols[rowptr[r] + s];
+          out.vals[at] = lvals[rowptr[r] + s];
+        } else {
+          out.cols[at] = r < n_local ? r : 0;
+        }
+      }
+    }
+  }
+}
+
 }  // namespace migmres

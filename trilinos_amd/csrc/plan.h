@@ -58,6 +58,18 @@ struct PairSell {
 };
 void make_pair_sell(int n_local, const long long *rowptr, const double *lvals, const PairPlan &plan, PairSell &out);
 
+// SELL-64 copy of a local CSR for the general SpMM kernel (k_spmm_sell): rows in chunks of
+// 64; chunk c holds its entries slot-major, entry s of row 64c + lane at
+// off[c] + s * 64 + lane for s < width[c] (the chunk's longest row); padding slots hold
+// column = the row itself and value 0 and are never summed (len[r] bounds the sum).
+struct Sell64 {
+  std::vector<long long> off;  // nchunks + 1
+  std::vector<int> len;        // n_local
+  std::vector<int> cols;
+  std::vector<double> vals;
+};
+void make_sell64(int n_local, const long long *rowptr, const int *lcols, const double *lvals, Sell64 &out);
+
 void galeri_rows(const std::string &kind, int nx, int ny, int nz, long long first, int n_local,
                  std::vector<long long> &rowptr, std::vector<long long> &gcols,
                  std::vector<double> &vals);

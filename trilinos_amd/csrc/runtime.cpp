@@ -647,6 +647,8 @@ void mv_assign(const migmres_mv &A, migmres_mv &Y) {
 // distributed CRS operator
 // ------------------------------------------------------------------------------------
 migmres_crs::~migmres_crs() {
+  for (void *p : {(void *)d_soff, (void *)d_slen, (void *)d_scol, (void *)d_sval})
+    if (p) hipFree(p);
   for (void *p : {(void *)d_rowptr, (void *)d_cols, (void *)d_export, (void *)d_vals, (void *)d_send,
                   (void *)d_ghost, (void *)d_psv, (void *)d_psk, (void *)d_psm, (void *)d_sel_int,
                   (void *)d_sel_bnd})
@@ -769,6 +771,24 @@ migmres_crs *crs_create(migmres_ctx *ctx, long long n_global, long long first, i
         A->pair_rmax = ps.rmax;
       }
     }
+    {
+      const char *ns = std::getenv("MIGMRES_NO_SELL_SPMM");
+      if (!A->use_pairs && !(ns && ns[0] == '1') && n_local > 0) {
+        Sell64 sp;
+        make_sell64(n_local, rowptr, lcols.data(), lvals.data(), sp);
+        MIG_HIP(hipMalloc(&A->d_soff, sizeof(long long) * sp.off.size()));
+        MIG_HIP(hipMalloc(&A->d_slen, sizeof(int) * sp.len.size()));
+        MIG_HIP(hipMalloc(&A->d_scol, sizeof(int) * (sp.cols.size() + 1)));
+        MIG_HIP(hipMalloc(&A->d_sval, sizeof(double) * (sp.vals.size() + 1)));
+        MIG_HIP(hipMemcpy(A->d_soff, sp.off.data(), sizeof(long long) * sp.off.size(), hipMemcpyHostToDevice));
+        MIG_HIP(hipMemcpy(A->d_slen, sp.len.data(), sizeof(int) * sp.len.size(), hipMemcpyHostToDevice));
+        if (!sp.cols.empty()) {
+          MIG_HIP(hipMemcpy(A->d_scol, sp.cols.data(), sizeof(int) * sp.cols.size(), hipMemcpyHostToDevice));
+          MIG_HIP(hipMemcpy(A->d_sval, sp.vals.data(), sizeof(double) * sp.vals.size(), hipMemcpyHostToDevice));
+        }
+        A->use_sell = true;
+      }
+    }
     if (n_remote > 0) {
       // interior / boundary units for the halo overlap (a unit is a row pair with the
       // row-pair kernel, else a row; boundary = reads at least one ghost column)
@@ -818,6 +838,9 @@ void crs_apply(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, double alpha,
     if (A.use_pairs)
       launch_spmm_pair(c->stream, A.n_local, A.pair_max_keys, A.pair_rmax, A.d_psv, A.d_psk, A.d_psm, X.desc(),
                        A.d_ghost, A.ldg, Y.desc(), alpha, beta, sel, nsel);
+    else if (A.use_sell)
+      launch_spmm_sell(c->stream, A.n_local, A.d_soff, A.d_slen, A.d_scol, A.d_sval, X.desc(), A.d_ghost, A.ldg,
+                       Y.desc(), alpha, beta, sel, nsel);
     else
       launch_spmm(c->stream, 0, A.n_local, A.d_rowptr, A.d_cols, A.d_vals, X.desc(), A.n_local, A.d_ghost, A.ldg,
                   Y.desc(), alpha, beta, sel, nsel);

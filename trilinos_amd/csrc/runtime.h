@@ -132,6 +132,11 @@ struct migmres_crs {
   unsigned short *d_psm = nullptr;
   bool use_pairs = false;
   int pair_max_keys = 0, pair_rmax = 0;
+  // SELL-64 copy for the general kernel (k_spmm_sell) when the pair plan does not apply
+  long long *d_soff = nullptr;
+  int *d_slen = nullptr, *d_scol = nullptr;
+  double *d_sval = nullptr;
+  bool use_sell = false;
   // interior / boundary split (units = pairs with the row-pair kernel, else rows): interior
   // units read no ghost column and run while the halo exchange is in flight
   int *d_sel_int = nullptr, *d_sel_bnd = nullptr;
