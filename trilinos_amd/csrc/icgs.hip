@@ -400,20 +400,28 @@ __global__ __launch_bounds__(256, 2) void k_nn_tn(MvDesc Q, int L, const double 
   }
 }
 
-// Wide variants for k <= 8 stage RW-row chunks (RW = 64: one 1024-thread workgroup per CU;
-// RW = 32: two 512-thread workgroups per CU), 256-512 B per Q column per visit instead of
-// 128 B: with 16-row chunks the Q stream alone, no compute, fell from 6.4 TB/s at L = 64 to
-// 3.7 TB/s at L = 200 (tools/mb_nntn.hip).
+// Wide variants for k <= 8 stage RW-row chunks (RW = 32: two 512-thread workgroups per CU;
+// RW = 64: one 1024-thread workgroup), 256-512 B per column per visit instead of 128 B: with
+// 16-row chunks the Q stream alone fell from 6.4 TB/s at L = 64 to 3.7 TB/s at L = 200
+// (tools/mb_nntn.hip, tools/mb_stream.hip).
+// The loader stages Q AND X (columns L .. L+k-1 of the staged image) with the same 16-byte
+// loads, so X needs no load of its own: a separate, conditional X load made the compiler
+// copy its register at the loop back-edge behind an s_waitcnt vmcnt(0), which drained the
+// next chunk's Q prefetch every iteration (5.1 -> see DESIGN.md section 4).
 //   phase 1: wave w = (row block rb = w % RB, K quarter kq = w / RB) forms a 16 x k partial
 //            of Qc C1; the 4 K quarters are summed in a fixed order by the X1 owners,
-//   X1:      thread t owns row t % RW of column t / RW (one load and one store per chunk),
+//   X1:      thread t owns row t % RW of column t / RW < k: X1 = X - D goes to HBM and back
+//            into the staged X column, which phase 2 reads as its B operand,
 //   phase 2: wave w accumulates Q tiles w, w + NWAVE, ... (16 columns each) against X1.
-// LDS: Qs[Lp][RW + 1] | Xs[RW][16] | red[NWAVE][NJ][64] | C1s[Lp][4 NJ]; 1-deep register
-// prefetch of the next chunk.
+// LDS: Qs[Lp][RW + 1] (Lp = round16(L + 4 NJ); columns past L + k stay zero) |
+//      red[NWAVE][NJ][64] | C1s[Lq][4 NJ] (Lq = round16(L), zero past L and k).
+// Workgroup b owns the contiguous chunk range [c0, c1): consecutive visits to a column are
+// adjacent pieces (tools/mb_stream.hip, 32-row chunks: 6.0-6.3 TB/s in this order against
+// 5.8-5.9 TB/s grid-stride).
 template <int RW>
 static size_t nw_lds_bytes(int L, int NJ) {
-  const int Lp = (L + 15) & ~15;
-  return sizeof(double) * ((size_t)Lp * (RW + 1) + RW * 16 + (RW / 4) * NJ * 64 + (size_t)Lp * 4 * NJ);
+  const int Lp = (L + 4 * NJ + 15) & ~15, Lq = (L + 15) & ~15;
+  return sizeof(double) * ((size_t)Lp * (RW + 1) + (RW / 4) * NJ * 64 + (size_t)Lq * 4 * NJ);
 }
 
 template <int RW, int NM, int NJ>
@@ -422,15 +430,15 @@ __global__ __launch_bounds__(16 * RW) void k_nn_tn_w(MvDesc Q, int L, const doub
                                                      double *__restrict__ sink) {
   constexpr int NTH = 16 * RW, NWAVE = NTH / 64, RB = RW / 16, LDQ = RW + 1, LPC = RW / 2;
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  const int Lp = (L + 15) & ~15;
+  const int LX = L + k;
+  const int Lp = (L + 4 * NJ + 15) & ~15, Lq = (L + 15) & ~15;
   double *Qs = sm;
-  double *Xs = sm + (size_t)Lp * LDQ;
-  double *red = Xs + RW * 16;
-  double *C1s = red + NWAVE * NJ * 64;  // [Lp][4 NJ], zero past L and k
+  double *red = Qs + (size_t)Lp * LDQ;
+  double *C1s = red + NWAVE * NJ * 64;
   const int t = threadIdx.x, w = t >> 6, l = t & 63, c = l & 15, g = l >> 4, n4 = l & 3;
   const int rb = w % RB, kq = w / RB;
-  for (int e = t; e < (Lp - L) * LDQ; e += NTH) Qs[L * LDQ + e] = 0.0;
-  for (int e = t; e < Lp * 4 * NJ; e += NTH) {
+  for (int e = t; e < Lp * LDQ; e += NTH) Qs[e] = 0.0;
+  for (int e = t; e < Lq * 4 * NJ; e += NTH) {
     const int i = e / (4 * NJ), j = e % (4 * NJ);
     C1s[e] = (i < L && j < k) ? C1[i + (long long)j * ldc] : 0.0;
   }
@@ -440,91 +448,102 @@ __global__ __launch_bounds__(16 * RW) void k_nn_tn_w(MvDesc Q, int L, const doub
 #pragma unroll
     for (int jg = 0; jg < NJ; ++jg) acc2[m][jg] = 0.0;
 
-  // loader: column lcol + 32 m (clamped), rows lrow, lrow + 1 of the chunk
+  // loader: staged column lcol + 32 m (clamped to LX - 1: duplicates rewrite the same
+  // value), rows lrow, lrow + 1 of the chunk; staged columns >= L come from X.
   const int lrow = 2 * (t % LPC), lcol = t / LPC;
-  auto scol = [&](int m) { const int i = lcol + 32 * m; return i < L ? i : L - 1; };
-  const double *qb = Q.base + lrow;
-  const long long qld = Q.ld;
-  // X1 owner: row xr of column xj (columns >= k store into the sink)
-  const int xr = t % RW, xj = t / RW;
-  const bool xok_col = xj < k;
-  const double *xsrc = colp_(X, xok_col ? xj : k - 1);
-  double *xdst = colp_(X, xok_col ? xj : k - 1);
-  const int xjg = (xj >> 2) < NJ ? (xj >> 2) : NJ - 1;
+  const double *lsrc[NM];
+  int lsts[NM];
+#pragma unroll
+  for (int m = 0; m < NM; ++m) {
+    int i = lcol + 32 * m;
+    i = i < LX ? i : LX - 1;
+    lsts[m] = i * LDQ + lrow;
+    lsrc[m] = (i < L ? Q.base + (long long)i * Q.ld : colp_(X, i - L)) + lrow;
+  }
+  // X1 element e = t mod (RW k): row xr of column xj.  Threads t >= RW k repeat an element
+  // and store the same value again, so the X1 store is unconditional: a conditional store
+  // makes the compiler drain the whole prefetch (vmcnt(0)) at the top of the next chunk.
+  const int xe = t % (RW * k), xr = xe % RW, xj = xe / RW;
+  const bool xprim = t < RW * k;
+  double *xdst = colp_(X, xj);
+  const int xjg = xj >> 2;
   const int xr16 = xr & 15, xrb = xr >> 4;
   const int xo = 16 * (xr16 & 3) + 4 * (xr16 >> 2) + (xj & 3);  // D lane of (row, column)
+  double *xs = Qs + (size_t)(L + xj) * LDQ + xr;
   const long long nchunks = (nrows + RW - 1) / RW;
-  const long long G = gridDim.x;
-  auto clampc = [&](long long chunk) { return chunk < nchunks ? chunk : nchunks - 1; };
+  const long long c0 = nchunks * blockIdx.x / gridDim.x, c1 = nchunks * (blockIdx.x + 1) / gridDim.x;
+  auto clampc = [&](long long chunk) { return chunk < c1 ? chunk : c1 - 1; };
 
+  // 1-deep register prefetch: the next chunk's loads are issued right after the barrier
+  // that publishes the current one and stay in flight through both phases.  Rows past nrows
+  // are zero padding in Q and X, so their X1 is zero and is stored back unguarded.
   d2 p[NM];
-  double xv;
-  {
-    const long long c0 = clampc(blockIdx.x);
 #pragma unroll
-    for (int m = 0; m < NM; ++m) p[m] = *(const d2 *)(qb + scol(m) * qld + c0 * RW);
-    xv = xsrc[c0 * RW + xr];
-  }
-  for (long long ch = blockIdx.x; ch < nchunks; ch += G) {
-    const long long r0 = ch * RW;
-#pragma unroll
-    for (int m = 0; m < NM; ++m) {
-      if (NT_DIAG_MASK & 4) {
-        Qs[scol(m) * LDQ + lrow] = p[m].x;
-        Qs[scol(m) * LDQ + lrow + 1] = p[m].y;
-      } else if (p[m].x == 12345.0) {
-        Qs[0] = p[m].y;
-      }
-    }
-    const double xcur = xv;
-    lds_barrier();
+  for (int m = 0; m < NM; ++m) p[m] = *(const d2 *)(lsrc[m] + c0 * RW);
+  // A store behind the prologue loads, like the X1 store behind the in-loop prefetch: the
+  // loop header then sees the same pending-event order on both incoming edges and waits
+  // vmcnt(1) for the last prefetched column instead of vmcnt(0) (which waits for the X1
+  // store's completion).  partial[0] of this workgroup is rewritten at the end.
+  if (NT_DIAG_MASK & 8) partial[(long long)blockIdx.x * L * k] = 0.0;
+  for (long long ch = c0; ch < c1; ++ch) {
     {
-      const long long cn = clampc(ch + G);
+      const long long r0 = ch * RW;
 #pragma unroll
-      for (int m = 0; m < NM; ++m) p[m] = *(const d2 *)(qb + scol(m) * qld + cn * RW);
-      if (NT_DIAG_MASK & 8) xv = xsrc[cn * RW + xr];
-    }
-    // phase 1: rows 16 rb .. 16 rb + 15, K steps s = kq + 4 m
-    double a1[NJ];
-#pragma unroll
-    for (int jg = 0; jg < NJ; ++jg) a1[jg] = 0.0;
-#pragma unroll
-    for (int m = 0; m < ((NT_DIAG_MASK & 1) ? 16 : 0); ++m) {
-      const int s = kq + 4 * m;
-      if (4 * s < L) {
-        const double qa = Qs[(4 * s + g) * LDQ + 16 * rb + c];
-#pragma unroll
-        for (int jg = 0; jg < NJ; ++jg) a1[jg] = mfma4(qa, C1s[(4 * s + g) * 4 * NJ + 4 * jg + n4], a1[jg]);
-      }
-    }
-#pragma unroll
-    for (int jg = 0; jg < NJ; ++jg) red[((kq * RB + rb) * NJ + jg) * 64 + l] = a1[jg];
-    lds_barrier();
-    {
-      const double d = (red[((0 * RB + xrb) * NJ + xjg) * 64 + xo] + red[((1 * RB + xrb) * NJ + xjg) * 64 + xo]) +
-                       (red[((2 * RB + xrb) * NJ + xjg) * 64 + xo] + red[((3 * RB + xrb) * NJ + xjg) * 64 + xo]);
-      const bool ok = xok_col && ch < nchunks && r0 + xr < nrows;
-      const double x1 = ok ? xcur - d : 0.0;
-      double *dst = ok ? xdst + r0 + xr : sink + (blockIdx.x * NTH + t);
-      if (NT_DIAG_MASK & 8) *dst = x1;
-      Xs[xr * 16 + xj] = x1;
-    }
-    lds_barrier();
-    // phase 2: tiles w, w + NWAVE, ... against the RW rows of X1
-#pragma unroll
-    for (int mm = 0; mm < ((NT_DIAG_MASK & 2) ? (16 + NWAVE - 1) / NWAVE : 0); ++mm) {
-      const int tt = w + NWAVE * mm;
-      if (16 * tt < L) {
-#pragma unroll
-        for (int s = 0; s < RW / 4; ++s) {
-          const double qa = Qs[(16 * tt + c) * LDQ + 4 * s + g];
-#pragma unroll
-          for (int jg = 0; jg < NJ; ++jg)
-            acc2[mm][jg] = mfma4(qa, Xs[(4 * s + g) * 16 + 4 * jg + n4], acc2[mm][jg]);
+      for (int m = 0; m < NM; ++m) {
+        if (NT_DIAG_MASK & 4) {
+          Qs[lsts[m]] = p[m].x;
+          Qs[lsts[m] + 1] = p[m].y;
+        } else if (p[m].x == 12345.0) {
+          Qs[0] = p[m].y;
         }
       }
+      lds_barrier();
+      {
+        const long long cn = clampc(ch + 1) * RW;
+#pragma unroll
+        for (int m = 0; m < NM; ++m) p[m] = *(const d2 *)(lsrc[m] + cn);
+      }
+      const double xval = *xs;
+      // phase 1: rows 16 rb .. 16 rb + 15, K steps s = kq + 4 m
+      double a1[NJ];
+#pragma unroll
+      for (int jg = 0; jg < NJ; ++jg) a1[jg] = 0.0;
+#pragma unroll
+      for (int m = 0; m < ((NT_DIAG_MASK & 1) ? 16 : 0); ++m) {
+        const int s = kq + 4 * m;
+        if (4 * s < L) {
+          const double qa = Qs[(4 * s + g) * LDQ + 16 * rb + c];
+#pragma unroll
+          for (int jg = 0; jg < NJ; ++jg) a1[jg] = mfma4(qa, C1s[(4 * s + g) * 4 * NJ + 4 * jg + n4], a1[jg]);
+        }
+      }
+#pragma unroll
+      for (int jg = 0; jg < NJ; ++jg) red[((kq * RB + rb) * NJ + jg) * 64 + l] = a1[jg];
+      lds_barrier();
+      {
+        const double d = (red[((0 * RB + xrb) * NJ + xjg) * 64 + xo] + red[((1 * RB + xrb) * NJ + xjg) * 64 + xo]) +
+                         (red[((2 * RB + xrb) * NJ + xjg) * 64 + xo] + red[((3 * RB + xrb) * NJ + xjg) * 64 + xo]);
+        const double x1 = xval - d;
+        if (NT_DIAG_MASK & 8) xdst[r0 + xr] = x1;
+        if (xprim) *xs = x1;
+      }
+      lds_barrier();
+      // phase 2: tiles w, w + NWAVE, ... against the RW rows of X1 (staged columns L + j)
+#pragma unroll
+      for (int mm = 0; mm < ((NT_DIAG_MASK & 2) ? (16 + NWAVE - 1) / NWAVE : 0); ++mm) {
+        const int tt = w + NWAVE * mm;
+        if (16 * tt < L) {
+#pragma unroll
+          for (int s = 0; s < RW / 4; ++s) {
+            const double qa = Qs[(16 * tt + c) * LDQ + 4 * s + g];
+#pragma unroll
+            for (int jg = 0; jg < NJ; ++jg)
+              acc2[mm][jg] = mfma4(qa, Qs[(L + 4 * jg + n4) * LDQ + 4 * s + g], acc2[mm][jg]);
+          }
+        }
+      }
+      lds_barrier();
     }
-    lds_barrier();
   }
   // partial (L x k) of this workgroup: tile tt rows 16 tt + 4 b + m
   double *out = partial + (long long)blockIdx.x * L * k;
@@ -565,9 +584,18 @@ static nt_kernel_t nt_pick(int L, int k) {
   }
 }
 
+#ifndef NT_WIDE_RW
+#define NT_WIDE_RW 32
+#endif
+#ifndef NT_WIDE_WGCU
+#define NT_WIDE_WGCU (NT_WIDE_RW == 32 ? 2 : 1)
+#endif
+constexpr int NW_RW = NT_WIDE_RW;  // rows per chunk of the wide variant (32: 2 WGs/CU, 64: 1 WG/CU)
+constexpr int NW_WG_PER_CU = NT_WIDE_WGCU;
+
 template <int RW, int NJ>
-static nt_kernel_t nw_pick_nm(int L) {
-  switch ((L + 31) >> 5) {
+static nt_kernel_t nw_pick_nm(int LX) {
+  switch ((LX + 31) >> 5) {
     case 1: return k_nn_tn_w<RW, 1, NJ>;
     case 2: return k_nn_tn_w<RW, 2, NJ>;
     case 3: return k_nn_tn_w<RW, 3, NJ>;
@@ -579,16 +607,11 @@ static nt_kernel_t nw_pick_nm(int L) {
   }
 }
 
-#ifndef NT_WIDE_RW
-#define NT_WIDE_RW 32
-#endif
-constexpr int NW_RW = NT_WIDE_RW;  // rows per chunk of the wide variant (32: 2 WGs/CU, 64: 1 WG/CU)
-constexpr int NW_WG_PER_CU = NW_RW == 32 ? 2 : 1;
 
 // The wide variant wins from L = 64 on (256^3, k = 8); below that the per-chunk latency
 // is not hidden.  It needs NW_WG_PER_CU workgroups' LDS to fit in 160 KiB.
 static bool nw_ok(int L, int k) {
-  return L >= 64 && k <= 8 && nw_lds_bytes<NW_RW>(L, (k + 3) >> 2) * NW_WG_PER_CU <= 160 * 1024;
+  return L >= 64 && k <= 8 && L + k <= 256 && nw_lds_bytes<NW_RW>(L, (k + 3) >> 2) * NW_WG_PER_CU <= 160 * 1024;
 }
 
 static int cu_count() {
@@ -628,10 +651,10 @@ void launch_nn_tn(hipStream_t s, MvDesc Q, int L, const double *C1, int ldc, MvD
   if (Q.cols) throw Error(MIGMRES_EINVAL, "nn_tn: Q must be a contiguous column range");
   if (nw_ok(L, k)) {
     const int NJ = (k + 3) >> 2;
-    nt_kernel_t f = NJ == 1 ? nw_pick_nm<NW_RW, 1>(L) : nw_pick_nm<NW_RW, 2>(L);
+    nt_kernel_t f = NJ == 1 ? nw_pick_nm<NW_RW, 1>(L + k) : nw_pick_nm<NW_RW, 2>(L + k);
     const size_t lds = nw_lds_bytes<NW_RW>(L, NJ);
     static bool attr_set[2][9] = {};
-    const int nm = (L + 31) >> 5;
+    const int nm = (L + k + 31) >> 5;
     if (!attr_set[NJ - 1][nm]) {
       if (hipFuncSetAttribute((const void *)f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
         throw Error(MIGMRES_EHIP, "nn_tn: cannot raise the dynamic LDS limit");
