@@ -1,3 +1,2 @@
 source ./tools_gpu_check.sh
-for v in a c; do step 60 mb_nntn_pf$v.log ./tools/mb_nntn_pf$v; done
-step 120 mb_lib.log ./tools/mb_lib 256 64
+for nb in 8 4 12 16 8; do step 120 mb_lib_nb$nb.log ./tools/mb_lib_nb$nb 256 64; done

@@ -22,22 +22,27 @@ void launch_reduce_small(hipStream_t s, const double *partial, int nblocks, int 
 void launch_gemm_nn_dot(hipStream_t s, MvDesc A, int L, const double *M, int ldm, MvDesc X,
                         int nrows, double alpha, double beta, int dmode, MvDesc D, double *partial,
                         int nblocks);
-// X1 = X - Q C1 in place and per-workgroup partials of Q^T X1 (L x k, column-major).
+// X1 = X - Q C1 and per-workgroup partials of Q^T X1 (L x k, column-major).  store_x1:
+// X1 is written back over X; otherwise X is left as it was (X1 lives only in the kernel,
+// and the closing update subtracts Q (C1 + C2) from the original X instead).
 // sink: scratch of nblocks * 256 doubles that absorbs the stores of padding lanes.
 bool nn_tn_supported(int L, int k);
 int nn_tn_blocks(int nrows, int L, int k);
 void launch_nn_tn(hipStream_t s, MvDesc Q, int L, const double *C1, int ldc, MvDesc X, int nrows,
-                  double *partial, int nblocks, double *sink);
+                  double *partial, int nblocks, double *sink, bool store_x1 = true);
 void launch_fb_a(hipStream_t s, MvDesc X, int j, const IcgsState *st, int nrows, double *partial, int nb);
 void launch_fb_b(hipStream_t s, MvDesc X, int j, const IcgsState *st, double *S, int nrows, double *partial, int nb);
 void launch_fb_c(hipStream_t s, MvDesc X, int j, const IcgsState *st, const double *S, int nrows, double *partial,
                  int nb);
 // Two-pass-per-column findBasis (see icgs.hip): a01 head, b2 = normalise previous column +
 // first update + second projection, ca = second update + next column's first projection.
+// rev = 1 sweeps the rows from the top down: consecutive passes alternate direction so each
+// pass starts on the rows the previous one touched last (still in the Infinity Cache).
 void launch_fb_a01(hipStream_t s, MvDesc X, int nrows, double *partial, int nb);
-void launch_fb_b2(hipStream_t s, MvDesc X, int j, const IcgsState *st, double *S, int nrows, double *partial, int nb);
-void launch_fb_ca(hipStream_t s, MvDesc X, int j, int has_next, const IcgsState *st, const double *S, int nrows,
-                  double *partial, int nb);
+void launch_fb_b2(hipStream_t s, MvDesc X, int j, const IcgsState *st, int nrows, double *partial, int nb,
+                  int rev = 0);
+void launch_fb_ca(hipStream_t s, MvDesc X, int j, int has_next, const IcgsState *st, int nrows, double *partial,
+                  int nb, int rev = 0);
 void launch_scale_col(hipStream_t s, MvDesc X, int j, const IcgsState *st, int nrows);
 // reduce_small followed by fb_scalar in one single-workgroup launch (single rank only)
 void launch_reduce_scalar(hipStream_t s, const double *partial, int nblocks, int nv, double *red, IcgsState *st,

@@ -59,6 +59,16 @@ int icgs_blocks(int nrows) {
   return b < 1 ? 1 : (b > 1024 ? 1024 : b);
 }
 
+// Store rows (r, r + 1) of a column: one 16-byte store, or only row r when r + 1 == nrows
+// (an odd tail).  Two 8-byte stores per lane would write every line in two halves.
+__device__ __forceinline__ void st_pair(double *p, double a, double b, bool two) {
+  if (two) {
+    *(d2 *)p = d2{a, b};
+  } else {
+    p[0] = a;
+  }
+}
+
 // out[o] = sum_b partial[b * nv + o], o < nv <= 17: one workgroup, every thread sums a
 // fixed subset of blocks for all outputs, then a fixed-shape tree (deterministic).
 __global__ __launch_bounds__(256) void k_reduce_small(const double *__restrict__ partial, int nblocks,
@@ -120,7 +130,10 @@ __global__ __launch_bounds__(256) void k_gemm_nn_dot(MvDesc A, int L, const doub
     for (int c = 0; c < KX; ++c) acc0[c] = acc1[c] = 0.0;
     // NB columns per step, all loads issued before the FMAs (more bytes in flight per wave);
     // rows past nrows are the zero padding of the multivector (ld > nrows), read unguarded.
-    constexpr int NB = 8;
+#ifndef NND_NB
+#define NND_NB 8
+#endif
+    constexpr int NB = NND_NB;
     int j = 0;
     for (; j + NB <= L; j += NB) {
       d2 v[NB];
@@ -155,11 +168,11 @@ __global__ __launch_bounds__(256) void k_gemm_nn_dot(MvDesc A, int L, const doub
           n0 = alpha * acc0[c];
           if (two) n1 = alpha * acc1[c];
         } else {
-          n0 = beta * xp[0] + alpha * acc0[c];
-          if (two) n1 = beta * xp[1] + alpha * acc1[c];
+          const d2 xo = *(const d2 *)xp;  // padding row of an odd tail reads zero
+          n0 = beta * xo.x + alpha * acc0[c];
+          if (two) n1 = beta * xo.y + alpha * acc1[c];
         }
-        xp[0] = n0;
-        if (two) xp[1] = n1;
+        st_pair(xp, n0, n1, two);
         if (dmode == 1 || dmode == 3) {
           dacc[c] += n0 * n0 + n1 * n1;
           if (dmode == 3) {
@@ -248,7 +261,7 @@ __device__ __forceinline__ double mfma4(double a, double b, double c) {
   return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
 }
 
-template <int NM, int NJ>
+template <int NM, int NJ, bool ST>
 __global__ __launch_bounds__(256, 2) void k_nn_tn(MvDesc Q, int L, const double *__restrict__ C1, int ldc,
                                                   MvDesc X, int k, int nrows, double *__restrict__ partial,
                                                   double *__restrict__ sink) {
@@ -349,7 +362,7 @@ __global__ __launch_bounds__(256, 2) void k_nn_tn(MvDesc Q, int L, const double 
       const bool ok = xcol_ok && live && r0 + xrow < nrows;
       const double x1 = ok ? xv - d : 0.0;
       double *dst = ok ? xdst + r0 + xrow : sink + (blockIdx.x * 256 + t);
-      if (NT_DIAG_MASK & 8) *dst = x1;
+      if ((NT_DIAG_MASK & 8) && ST) *dst = x1;
       Xs[xrow * 16 + xc] = x1;
       if (NT_DIAG_MASK & 8) loadx(xv, chunk + 2 * G);
     }
@@ -424,7 +437,7 @@ static size_t nw_lds_bytes(int L, int NJ) {
   return sizeof(double) * ((size_t)Lp * (RW + 1) + (RW / 4) * NJ * 64 + (size_t)Lq * 4 * NJ);
 }
 
-template <int RW, int NM, int NJ>
+template <int RW, int NM, int NJ, bool ST>
 __global__ __launch_bounds__(16 * RW) void k_nn_tn_w(MvDesc Q, int L, const double *__restrict__ C1, int ldc,
                                                      MvDesc X, int k, int nrows, double *__restrict__ partial,
                                                      double *__restrict__ sink) {
@@ -484,7 +497,7 @@ __global__ __launch_bounds__(16 * RW) void k_nn_tn_w(MvDesc Q, int L, const doub
   // loop header then sees the same pending-event order on both incoming edges and waits
   // vmcnt(1) for the last prefetched column instead of vmcnt(0) (which waits for the X1
   // store's completion).  partial[0] of this workgroup is rewritten at the end.
-  if (NT_DIAG_MASK & 8) partial[(long long)blockIdx.x * L * k] = 0.0;
+  if ((NT_DIAG_MASK & 8) && ST) partial[(long long)blockIdx.x * L * k] = 0.0;
   for (long long ch = c0; ch < c1; ++ch) {
     {
       const long long r0 = ch * RW;
@@ -524,7 +537,7 @@ __global__ __launch_bounds__(16 * RW) void k_nn_tn_w(MvDesc Q, int L, const doub
         const double d = (red[((0 * RB + xrb) * NJ + xjg) * 64 + xo] + red[((1 * RB + xrb) * NJ + xjg) * 64 + xo]) +
                          (red[((2 * RB + xrb) * NJ + xjg) * 64 + xo] + red[((3 * RB + xrb) * NJ + xjg) * 64 + xo]);
         const double x1 = xval - d;
-        if (NT_DIAG_MASK & 8) xdst[r0 + xr] = x1;
+        if ((NT_DIAG_MASK & 8) && ST) xdst[r0 + xr] = x1;
         if (xprim) *xs = x1;
       }
       lds_barrier();
@@ -561,26 +574,27 @@ __global__ __launch_bounds__(16 * RW) void k_nn_tn_w(MvDesc Q, int L, const doub
 
 typedef void (*nt_kernel_t)(MvDesc, int, const double *, int, MvDesc, int, int, double *, double *);
 
-template <int NJ>
+template <int NJ, bool ST>
 static nt_kernel_t nt_pick_nm(int L) {
   switch ((L + 31) >> 5) {
-    case 1: return k_nn_tn<1, NJ>;
-    case 2: return k_nn_tn<2, NJ>;
-    case 3: return k_nn_tn<3, NJ>;
-    case 4: return k_nn_tn<4, NJ>;
-    case 5: return k_nn_tn<5, NJ>;
-    case 6: return k_nn_tn<6, NJ>;
-    case 7: return k_nn_tn<7, NJ>;
-    default: return k_nn_tn<8, NJ>;
+    case 1: return k_nn_tn<1, NJ, ST>;
+    case 2: return k_nn_tn<2, NJ, ST>;
+    case 3: return k_nn_tn<3, NJ, ST>;
+    case 4: return k_nn_tn<4, NJ, ST>;
+    case 5: return k_nn_tn<5, NJ, ST>;
+    case 6: return k_nn_tn<6, NJ, ST>;
+    case 7: return k_nn_tn<7, NJ, ST>;
+    default: return k_nn_tn<8, NJ, ST>;
   }
 }
 
+template <bool ST>
 static nt_kernel_t nt_pick(int L, int k) {
   switch ((k + 3) >> 2) {
-    case 1: return nt_pick_nm<1>(L);
-    case 2: return nt_pick_nm<2>(L);
-    case 3: return nt_pick_nm<3>(L);
-    default: return nt_pick_nm<4>(L);
+    case 1: return nt_pick_nm<1, ST>(L);
+    case 2: return nt_pick_nm<2, ST>(L);
+    case 3: return nt_pick_nm<3, ST>(L);
+    default: return nt_pick_nm<4, ST>(L);
   }
 }
 
@@ -593,17 +607,17 @@ static nt_kernel_t nt_pick(int L, int k) {
 constexpr int NW_RW = NT_WIDE_RW;  // rows per chunk of the wide variant (32: 2 WGs/CU, 64: 1 WG/CU)
 constexpr int NW_WG_PER_CU = NT_WIDE_WGCU;
 
-template <int RW, int NJ>
+template <int RW, int NJ, bool ST>
 static nt_kernel_t nw_pick_nm(int LX) {
   switch ((LX + 31) >> 5) {
-    case 1: return k_nn_tn_w<RW, 1, NJ>;
-    case 2: return k_nn_tn_w<RW, 2, NJ>;
-    case 3: return k_nn_tn_w<RW, 3, NJ>;
-    case 4: return k_nn_tn_w<RW, 4, NJ>;
-    case 5: return k_nn_tn_w<RW, 5, NJ>;
-    case 6: return k_nn_tn_w<RW, 6, NJ>;
-    case 7: return k_nn_tn_w<RW, 7, NJ>;
-    default: return k_nn_tn_w<RW, 8, NJ>;
+    case 1: return k_nn_tn_w<RW, 1, NJ, ST>;
+    case 2: return k_nn_tn_w<RW, 2, NJ, ST>;
+    case 3: return k_nn_tn_w<RW, 3, NJ, ST>;
+    case 4: return k_nn_tn_w<RW, 4, NJ, ST>;
+    case 5: return k_nn_tn_w<RW, 5, NJ, ST>;
+    case 6: return k_nn_tn_w<RW, 6, NJ, ST>;
+    case 7: return k_nn_tn_w<RW, 7, NJ, ST>;
+    default: return k_nn_tn_w<RW, 8, NJ, ST>;
   }
 }
 
@@ -633,7 +647,7 @@ int nn_tn_blocks(int nrows, int L, int k) {
     return b < 1 ? 1 : (int)b;
   }
   int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nt_pick(L, k), 256, nt_lds_bytes(L)) != hipSuccess ||
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nt_pick<true>(L, k), 256, nt_lds_bytes(L)) != hipSuccess ||
       per_cu < 1)
     per_cu = 2;
   const long long nchunks = (nrows + NT_ROWS - 1) / NT_ROWS;
@@ -645,25 +659,26 @@ int nn_tn_blocks(int nrows, int L, int k) {
 bool nn_tn_supported(int L, int k) { return L >= 1 && L <= NT_MAXL && k >= 1 && k <= 16; }
 
 void launch_nn_tn(hipStream_t s, MvDesc Q, int L, const double *C1, int ldc, MvDesc X, int nrows,
-                  double *partial, int nblocks, double *sink) {
+                  double *partial, int nblocks, double *sink, bool store_x1) {
   const int k = X.ncols;
   if (!nn_tn_supported(L, k)) throw Error(MIGMRES_EINVAL, "nn_tn: 1 <= L <= 256 and 1 <= k <= 16");
   if (Q.cols) throw Error(MIGMRES_EINVAL, "nn_tn: Q must be a contiguous column range");
   if (nw_ok(L, k)) {
     const int NJ = (k + 3) >> 2;
-    nt_kernel_t f = NJ == 1 ? nw_pick_nm<NW_RW, 1>(L + k) : nw_pick_nm<NW_RW, 2>(L + k);
+    nt_kernel_t f = store_x1 ? (NJ == 1 ? nw_pick_nm<NW_RW, 1, true>(L + k) : nw_pick_nm<NW_RW, 2, true>(L + k))
+                             : (NJ == 1 ? nw_pick_nm<NW_RW, 1, false>(L + k) : nw_pick_nm<NW_RW, 2, false>(L + k));
     const size_t lds = nw_lds_bytes<NW_RW>(L, NJ);
-    static bool attr_set[2][9] = {};
+    static bool attr_set[2][2][9] = {};
     const int nm = (L + k + 31) >> 5;
-    if (!attr_set[NJ - 1][nm]) {
+    if (!attr_set[store_x1][NJ - 1][nm]) {
       if (hipFuncSetAttribute((const void *)f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
         throw Error(MIGMRES_EHIP, "nn_tn: cannot raise the dynamic LDS limit");
-      attr_set[NJ - 1][nm] = true;
+      attr_set[store_x1][NJ - 1][nm] = true;
     }
     hipLaunchKernelGGL(f, dim3(nblocks), dim3(16 * NW_RW), lds, s, Q, L, C1, ldc, X, k, nrows, partial, sink);
   } else {
-    hipLaunchKernelGGL(nt_pick(L, k), dim3(nblocks), dim3(256), nt_lds_bytes(L), s, Q, L, C1, ldc, X, k, nrows,
-                       partial, sink);
+    hipLaunchKernelGGL(store_x1 ? nt_pick<true>(L, k) : nt_pick<false>(L, k), dim3(nblocks), dim3(256),
+                       nt_lds_bytes(L), s, Q, L, C1, ldc, X, k, nrows, partial, sink);
   }
   LAUNCH_CHECK_();
 }
@@ -689,8 +704,7 @@ __global__ __launch_bounds__(256) void k_fb_a(MvDesc X, int j, const IcgsState *
     if (j > 0) {
       const d2 p = *(const d2 *)(xp + r);
       const double q0 = invp * p.x, q1 = invp * p.y;
-      xp[r] = q0;
-      if (r + 1 < nrows) xp[r + 1] = q1;
+      st_pair(xp + r, q0, q1, r + 1 < nrows);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         if (i < j - 1) {
@@ -730,8 +744,7 @@ __global__ __launch_bounds__(256) void k_fb_b(MvDesc X, int j, const IcgsState *
       }
     const d2 x = *(const d2 *)(xj + r);
     const double a0 = x.x - t0, a1 = x.y - t1;
-    S[r] = a0;
-    if (r + 1 < nrows) S[r + 1] = a1;
+    st_pair(S + r, a0, a1, r + 1 < nrows);
 #pragma unroll
     for (int i = 0; i < 16; ++i)
       if (i < j) v[i] += q[i].x * a0 + q[i].y * a1;
@@ -762,8 +775,7 @@ __global__ __launch_bounds__(256) void k_fb_c(MvDesc X, int j, const IcgsState *
     const d2 old = *(const d2 *)(xj + r);
     const double a0 = sv.x - t0, a1 = sv.y - t1;
     v[0] += a0 * old.x + a1 * old.y;
-    xj[r] = a0;
-    if (r + 1 < nrows) xj[r + 1] = a1;
+    st_pair(xj + r, a0, a1, r + 1 < nrows);
   }
   block_reduce_store<1>(v, 1, partial);
 }
@@ -771,8 +783,12 @@ __global__ __launch_bounds__(256) void k_fb_c(MvDesc X, int j, const IcgsState *
 // Two passes per column instead of three.  The first projection of column j+1 onto the
 // basis is accumulated in the same pass that finishes column j (k_fb_ca), against column j
 // before its normalisation: <x2_j, X_{j+1}> is scaled by 1/diag_j afterwards (k_fb_scalar
-// stage 6), and column j is normalised on the fly by the next pass (k_fb_b2), which also
-// writes it back -- the same x2_j * (1/diag_j) the reference stores.
+// stage 6).  Column j - 1 stays unnormalised in memory until the pass that finishes column
+// j (k_fb_ca) writes it back as x2_{j-1} * (1/diag_{j-1}) -- the value the reference stores
+// -- and both passes of column j apply that scaling to it on the fly.  The first update
+// x1 = X_j - sum_i X_i P_i is not stored between the passes: k_fb_ca recomputes it with the
+// same operations in the same order (bit-identical), which saves writing and re-reading a
+// column per step; k_fb_b2 is read-only.
 //
 // (a01) partials [oldDot_0, oldDot_1, <X_0, X_1>] with X_0 not yet normalised.
 __global__ __launch_bounds__(256) void k_fb_a01(MvDesc X, int nrows, double *__restrict__ partial) {
@@ -789,11 +805,10 @@ __global__ __launch_bounds__(256) void k_fb_a01(MvDesc X, int nrows, double *__r
   block_reduce_store<3>(v, 3, partial);
 }
 
-// (b2) normalise column j-1 in place (x * inv[j-1]); x1 = X_j - sum_i X_i P_i -> S;
-// partials <X_i, x1> (i < j) and <x1, x1> (index j, the DGKS re-orthogonalisation test),
-// X_{j-1} taken normalised.
-__global__ __launch_bounds__(256) void k_fb_b2(MvDesc X, int j, const IcgsState *__restrict__ st,
-                                               double *__restrict__ S, int nrows, double *__restrict__ partial) {
+// (b2) x1 = X_j - sum_i X_i P_i with X_{j-1} scaled by inv[j-1]; partials <X_i, x1> (i < j)
+// and <x1, x1> (index j, the DGKS re-orthogonalisation test).  Writes nothing.
+__global__ __launch_bounds__(256) void k_fb_b2(MvDesc X, int j, const IcgsState *__restrict__ st, int nrows,
+                                               double *__restrict__ partial, int rev) {
   double v[17];
   double P[16];
   v[16] = 0.0;
@@ -804,9 +819,9 @@ __global__ __launch_bounds__(256) void k_fb_b2(MvDesc X, int j, const IcgsState 
   }
   const double invp = st->inv[j - 1];
   const double *xj = colp_(X, j);
-  double *xprev = colp_(X, j - 1);
-  for (long long r = 2LL * ((long long)blockIdx.x * 256 + threadIdx.x); r < nrows;
-       r += 2LL * gridDim.x * 256) {
+  const long long np = (nrows + 1) / 2;
+  for (long long pp = (long long)blockIdx.x * 256 + threadIdx.x; pp < np; pp += (long long)gridDim.x * 256) {
+    const long long r = 2 * (rev ? np - 1 - pp : pp);
     d2 q[16];
     double t0 = 0.0, t1 = 0.0;
 #pragma unroll
@@ -820,17 +835,8 @@ __global__ __launch_bounds__(256) void k_fb_b2(MvDesc X, int j, const IcgsState 
         t0 += q[i].x * P[i];
         t1 += q[i].y * P[i];
       }
-    // write the normalised column back (the padding row of an odd tail is not written)
-#pragma unroll
-    for (int i = 0; i < 16; ++i)
-      if (i == j - 1) {
-        xprev[r] = q[i].x;
-        if (r + 1 < nrows) xprev[r + 1] = q[i].y;
-      }
     const d2 x = *(const d2 *)(xj + r);
     const double a0 = x.x - t0, a1 = x.y - t1;
-    S[r] = a0;
-    if (r + 1 < nrows) S[r + 1] = a1;
 #pragma unroll
     for (int i = 0; i < 16; ++i)
       if (i < j) v[i] += q[i].x * a0 + q[i].y * a1;
@@ -841,36 +847,56 @@ __global__ __launch_bounds__(256) void k_fb_b2(MvDesc X, int j, const IcgsState 
   block_reduce_store<17>(v, j + 1, partial);
 }
 
-// (ca) x2 = S - sum_i X_i P2_i -> X_j (not normalised); partials
-// [newDot_j = <x2, X_j old>, and if j + 1 < k: oldDot_{j+1}, <X_i, X_{j+1}> (i < j), <x2, X_{j+1}>]
+// (ca) x1 as in (b2), x2 = x1 - sum_i X_i P2_i -> X_j (not normalised), X_{j-1} * inv[j-1]
+// -> X_{j-1}; partials [newDot_j = <x2, X_j old>, and if j + 1 < k: oldDot_{j+1},
+// <X_i, X_{j+1}> (i < j), <x2, X_{j+1}>]
 __global__ __launch_bounds__(256) void k_fb_ca(MvDesc X, int j, int has_next, const IcgsState *__restrict__ st,
-                                               const double *__restrict__ S, int nrows,
-                                               double *__restrict__ partial) {
+                                               int nrows, double *__restrict__ partial, int rev) {
   double v[17];
 #pragma unroll
   for (int i = 0; i < 17; ++i) v[i] = 0.0;
-  double P[16];
+  double P[16], P2[16];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) P[i] = i < j ? st->P2[i] : 0.0;
+  for (int i = 0; i < 16; ++i) {
+    P[i] = i < j ? st->P[i] : 0.0;
+    P2[i] = i < j ? st->P2[i] : 0.0;
+  }
+  const double invp = st->inv[j - 1];
   double *xj = colp_(X, j);
+  double *xprev = colp_(X, j - 1);
   const double *xn = colp_(X, has_next ? j + 1 : j);
-  for (long long r = 2LL * ((long long)blockIdx.x * 256 + threadIdx.x); r < nrows;
-       r += 2LL * gridDim.x * 256) {
+  const long long np = (nrows + 1) / 2;
+  for (long long pp = (long long)blockIdx.x * 256 + threadIdx.x; pp < np; pp += (long long)gridDim.x * 256) {
+    const long long r = 2 * (rev ? np - 1 - pp : pp);
+    const bool two = r + 1 < nrows;
     d2 q[16];
     double t0 = 0.0, t1 = 0.0;
 #pragma unroll
     for (int i = 0; i < 16; ++i)
       if (i < j) {
         q[i] = *(const d2 *)(colp_(X, i) + r);
+        if (i == j - 1) {
+          q[i].x = invp * q[i].x;
+          q[i].y = invp * q[i].y;
+        }
         t0 += q[i].x * P[i];
         t1 += q[i].y * P[i];
       }
-    const d2 sv = *(const d2 *)(S + r);
     const d2 old = *(const d2 *)(xj + r);
-    const double a0 = sv.x - t0, a1 = sv.y - t1;
+    const double s0 = old.x - t0, s1 = old.y - t1;
+    double u0 = 0.0, u1 = 0.0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (i < j) {
+        u0 += q[i].x * P2[i];
+        u1 += q[i].y * P2[i];
+      }
+    const double a0 = s0 - u0, a1 = s1 - u1;
     v[0] += a0 * old.x + a1 * old.y;
-    xj[r] = a0;
-    if (r + 1 < nrows) xj[r + 1] = a1;
+    st_pair(xj + r, a0, a1, two);
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (i == j - 1) st_pair(xprev + r, q[i].x, q[i].y, two);
     if (has_next) {
       const d2 nx = *(const d2 *)(xn + r);
       v[1] += nx.x * nx.x + nx.y * nx.y;
@@ -1088,13 +1114,14 @@ void launch_fb_a01(hipStream_t s, MvDesc X, int nrows, double *partial, int nb) 
   k_fb_a01<<<nb, 256, 0, s>>>(X, nrows, partial);
   LAUNCH_CHECK_();
 }
-void launch_fb_b2(hipStream_t s, MvDesc X, int j, const IcgsState *st, double *S, int nrows, double *partial, int nb) {
-  k_fb_b2<<<nb, 256, 0, s>>>(X, j, st, S, nrows, partial);
+void launch_fb_b2(hipStream_t s, MvDesc X, int j, const IcgsState *st, int nrows, double *partial, int nb,
+                  int rev) {
+  k_fb_b2<<<nb, 256, 0, s>>>(X, j, st, nrows, partial, rev);
   LAUNCH_CHECK_();
 }
-void launch_fb_ca(hipStream_t s, MvDesc X, int j, int has_next, const IcgsState *st, const double *S, int nrows,
-                  double *partial, int nb) {
-  k_fb_ca<<<nb, 256, 0, s>>>(X, j, has_next, st, S, nrows, partial);
+void launch_fb_ca(hipStream_t s, MvDesc X, int j, int has_next, const IcgsState *st, int nrows, double *partial,
+                  int nb, int rev) {
+  k_fb_ca<<<nb, 256, 0, s>>>(X, j, has_next, st, nrows, partial, rev);
   LAUNCH_CHECK_();
 }
 void launch_scale_col(hipStream_t s, MvDesc X, int j, const IcgsState *st, int nrows) {

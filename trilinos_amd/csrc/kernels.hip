@@ -658,12 +658,19 @@ __global__ __launch_bounds__(256) void k_gemm_nn(MvDesc A, int L, const double *
   for (int c = 0; c < KX; ++c) {
     if (c < kx) {
       double *xp = colp(X, c) + r;
+      double n0, n1;
       if (beta == 0.0) {
-        xp[0] = alpha * acc0[c];
-        if (two) xp[1] = alpha * acc1[c];
+        n0 = alpha * acc0[c];
+        n1 = alpha * acc1[c];
       } else {
-        xp[0] = beta * xp[0] + alpha * acc0[c];
-        if (two) xp[1] = beta * xp[1] + alpha * acc1[c];
+        const d2 xo = *(const d2 *)xp;  // padding row of an odd tail reads zero
+        n0 = beta * xo.x + alpha * acc0[c];
+        n1 = beta * xo.y + alpha * acc1[c];
+      }
+      if (two) {  // one 16-byte store per lane (two 8-byte stores write every line in halves)
+        *(d2 *)xp = d2{n0, n1};
+      } else {
+        xp[0] = n0;
       }
     }
   }

@@ -289,6 +289,8 @@ struct FastIcgs {
   MvPtr tmpX;
   long long calls = 0, fallbacks = 0;
   bool use_fused = true;  // MIGMRES_NO_FUSED_NN_TN=1 selects the two-kernel form (A/B timing)
+  int fb_rev = 1;         // findBasis b2 passes sweep rows top-down (MIGMRES_FB_REV=0: all bottom-up)
+  bool x1_store = false;  // fused pass writes X1 back (MIGMRES_NN_TN_STORE=1, A/B timing)
   int nt_cache[257][4] = {};
 
   ~FastIcgs() { release(); }
@@ -320,6 +322,10 @@ struct FastIcgs {
       for (int &v : row) v = 0;
     const char *nf = std::getenv("MIGMRES_NO_FUSED_NN_TN");
     use_fused = !(nf && nf[0] == '1');
+    const char *fr = std::getenv("MIGMRES_FB_REV");
+    fb_rev = !(fr && fr[0] == '0');
+    const char *xs = std::getenv("MIGMRES_NN_TN_STORE");
+    x1_store = xs && xs[0] == '1';
     const size_t np = std::max({(size_t)nblk_tn * 512 * 16, (size_t)nblk_ic * 17,
                                 (size_t)nn_tn_blocks(nl, 16, 1) * 256 * 16});
     MIG_HIP(hipMalloc(&partial, sizeof(double) * np));
@@ -389,27 +395,32 @@ struct FastIcgs {
     launch_gemm_nn_dot(ctx->stream, Q, L, M, ldm, X, n_local, -1.0, 1.0, dot, X, partial, nblk_ic);
   }
 
-  // X = X - Q C1 (C1 leading dim ldc1) then out = Q^T X, summed over ranks: one fused pass
-  // over Q when the shape allows it, else MvTimesMatAddMv followed by MvTransMv.
-  void nn_then_tn(const MvDesc &Q, int L, const double *C1, int ldc1, const MvDesc &X, int k, double *out) {
+  // X1 = X - Q C1 (C1 leading dim ldc1) then out = Q^T X1, summed over ranks: one fused pass
+  // over Q when the shape allows it, else MvTimesMatAddMv followed by MvTransMv.  Returns
+  // whether X now holds X1.  The fused pass leaves X unchanged unless x1_store is set: the
+  // caller's closing update then forms X - Q (C1 + C2) from the original X, so the pass is
+  // read-only (a k-column write in a read stream costs far more than its bytes:
+  // tools/mb_rw.hip, 6.2 TB/s read-only against 5.0 TB/s with the write at L = 104).
+  bool nn_then_tn(const MvDesc &Q, int L, const double *C1, int ldc1, const MvDesc &X, int k, double *out) {
     // Measured at 256^3, k = 8 (tools/mb_lib.cpp): the fused kernel beats the two streaming
     // kernels from L = 16 on (1.3 vs 1.4 ms at L = 16, 9.0 vs 10.5 ms at L = 200).
     const bool fused_wins = L >= 16;
     if (use_fused && fused_wins && !Q.cols && nn_tn_supported(L, k)) {
       const int nb = nt_blocks(L, k);
       {
-        ProfScope ps(ctx, K_NN_TN, 8.0 * n_local * (L + 2.0 * k) + 8.0 * nb * L * k);
-        launch_nn_tn(ctx->stream, Q, L, C1, ldc1, X, n_local, partial, nb, sink);
+        ProfScope ps(ctx, K_NN_TN, 8.0 * n_local * (L + (x1_store ? 2.0 : 1.0) * k) + 8.0 * nb * L * k);
+        launch_nn_tn(ctx->stream, Q, L, C1, ldc1, X, n_local, partial, nb, sink, x1_store);
       }
       {
         ProfScope ps(ctx, K_REDUCE, 8.0 * nb * L * k);
         launch_reduce_partials_ld(ctx->stream, partial, nb, L, k, L, 1.0, out);
       }
       allreduce(out, (size_t)L * k);
-      return;
+      return x1_store;
     }
     nn(Q, L, C1, ldc1, X, k, 0);
     tn(Q, L, X, k, out, L);
+    return true;
   }
 
   int nt_blocks(int L, int k) {
@@ -440,14 +451,14 @@ struct FastIcgs {
       }
       for (int j = 1; j < k; ++j) {
         {
-          ProfScope ps(ctx, K_FB, 8.0 * n * (j + 3));
-          launch_fb_b2(ctx->stream, X, j, st, S, n_local, partial, nblk_ic);
+          ProfScope ps(ctx, K_FB, 8.0 * n * (j + 1));
+          launch_fb_b2(ctx->stream, X, j, st, n_local, partial, nblk_ic, fb_rev);
         }
         reduce_scalar(j + 1, 1, j, k, complete);
         const int has_next = j + 1 < k;
         {
           ProfScope ps(ctx, K_FB, 8.0 * n * (j + 3 + has_next));
-          launch_fb_ca(ctx->stream, X, j, has_next, st, S, n_local, partial, nblk_ic);
+          launch_fb_ca(ctx->stream, X, j, has_next, st, n_local, partial, nblk_ic, 0);
         }
         reduce_scalar(has_next ? j + 3 : 1, 6, j, k, complete);
       }
@@ -490,14 +501,14 @@ struct FastIcgs {
     const MvDesc xd = X.desc(), qd = Q.desc();
     if (k == 1) {  // blkOrtho1, then MvDot and MvScale
       tn(qd, L, xd, 1, R1, L);
-      nn_then_tn(qd, L, R1, L, xd, 1, R2);
-      nn(qd, L, R2, L, xd, 1, 1);
+      const bool x1 = nn_then_tn(qd, L, R1, L, xd, 1, R2);
+      launch_add_coef(ctx->stream, R1, L, R2, L, Cout, L, L, 1);
+      nn(qd, L, x1 ? R2 : Cout, L, xd, 1, 1);
       reduce_scalar(1, 4, 0, 1, 0);
       {
         ProfScope ps(ctx, K_SCALE, 16.0 * n_local);
         launch_scale_col(ctx->stream, xd, 0, st, n_local);
       }
-      launch_add_coef(ctx->stream, R1, L, R2, L, Cout, L, L, 1);
       fetch(L, 1);
       for (int i = 0; i < L; ++i) C[i] = hC()[i];
       B[0] = hst().B[0];
@@ -516,10 +527,11 @@ struct FastIcgs {
       allreduce(R1, (size_t)(L + k) * k);
     }
     launch_blk_old(ctx->stream, st, R1, L + k, L, k);
-    nn_then_tn(qd, L, R1, L + k, xd, k, R2);
-    nn(qd, L, R2, L, xd, k, 3);
-    reduce_scalar(k + 1, 3, 0, k, 0);
+    const bool x1 = nn_then_tn(qd, L, R1, L + k, xd, k, R2);
     launch_add_coef(ctx->stream, R1, L + k, R2, L, Cout, L, L, k);
+    // X2 = X1 - Q C2 (reference order) when X holds X1, else X - Q (C1 + C2)
+    nn(qd, L, x1 ? R2 : Cout, L, xd, k, 3);
+    reduce_scalar(k + 1, 3, 0, k, 0);
     find_basis(xd, k, 0, true);
     fetch(L, k);
     const IcgsState &s = hst();
