@@ -3,6 +3,5 @@ step 600 pytest_gpu.log python -u -m pytest tests -m gpu -x -q --timeout 120 --t
 B="python bench.py --no-cpu-baseline"
 for i in 1 2; do
   step 300 ab_old_$i.json bash -c "cd ab_old && $B"
-  step 300 ab_fb_$i.json env MIGMRES_NN_TN_STORE=1 $B
   step 300 ab_new_$i.json $B
 done

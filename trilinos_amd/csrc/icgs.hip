@@ -805,110 +805,142 @@ __global__ __launch_bounds__(256) void k_fb_a01(MvDesc X, int nrows, double *__r
   block_reduce_store<3>(v, 3, partial);
 }
 
+// The column index j is a template parameter (k <= 16): the per-thread arrays hold exactly
+// the j prior columns, and each thread takes U row pairs (one grid stride apart, so every
+// wave-instruction still reads 1 KB contiguous per column) with all their loads issued
+// before the arithmetic -- (j + 1) U 16-byte loads in flight per thread.  With one pair per
+// thread the j = 1 pass had two loads in flight per thread.
+template <int J>
+struct FbU {
+  static constexpr int U = J <= 2 ? 4 : J <= 5 ? 2 : 1;
+};
+
+// Row pair u of this thread's group starting at pair p0: the global pair (reversed when
+// rev), clamped to a valid pair when past the end (ok = false: loaded, not used).
+__device__ __forceinline__ long long fb_pair(long long p0, int u, long long stride, long long np, int rev,
+                                             bool &ok) {
+  const long long pu = p0 + u * stride;
+  ok = pu < np;
+  const long long pc = ok ? pu : np - 1;
+  return 2 * (rev ? np - 1 - pc : pc);
+}
+
 // (b2) x1 = X_j - sum_i X_i P_i with X_{j-1} scaled by inv[j-1]; partials <X_i, x1> (i < j)
 // and <x1, x1> (index j, the DGKS re-orthogonalisation test).  Writes nothing.
-__global__ __launch_bounds__(256) void k_fb_b2(MvDesc X, int j, const IcgsState *__restrict__ st, int nrows,
+template <int J>
+__global__ __launch_bounds__(256) void k_fb_b2(MvDesc X, const IcgsState *__restrict__ st, int nrows,
                                                double *__restrict__ partial, int rev) {
-  double v[17];
-  double P[16];
-  v[16] = 0.0;
+  constexpr int U = FbU<J>::U;
+  double v[J + 1];
+  double P[J];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    v[i] = 0.0;
-    P[i] = i < j ? st->P[i] : 0.0;
-  }
-  const double invp = st->inv[j - 1];
-  const double *xj = colp_(X, j);
-  const long long np = (nrows + 1) / 2;
-  for (long long pp = (long long)blockIdx.x * 256 + threadIdx.x; pp < np; pp += (long long)gridDim.x * 256) {
-    const long long r = 2 * (rev ? np - 1 - pp : pp);
-    d2 q[16];
-    double t0 = 0.0, t1 = 0.0;
+  for (int i = 0; i <= J; ++i) v[i] = 0.0;
 #pragma unroll
-    for (int i = 0; i < 16; ++i)
-      if (i < j) {
-        q[i] = *(const d2 *)(colp_(X, i) + r);
-        if (i == j - 1) {
-          q[i].x = invp * q[i].x;
-          q[i].y = invp * q[i].y;
-        }
-        t0 += q[i].x * P[i];
-        t1 += q[i].y * P[i];
+  for (int i = 0; i < J; ++i) P[i] = st->P[i];
+  const double invp = st->inv[J - 1];
+  const double *xc[J + 1];
+#pragma unroll
+  for (int i = 0; i <= J; ++i) xc[i] = colp_(X, i);
+  const long long np = (nrows + 1) / 2, stride = (long long)gridDim.x * 256;
+  for (long long p0 = (long long)blockIdx.x * 256 + threadIdx.x; p0 < np; p0 += U * stride) {
+    d2 q[U][J + 1];
+    bool ok[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long r = fb_pair(p0, u, stride, np, rev, ok[u]);
+#pragma unroll
+      for (int i = 0; i <= J; ++i) q[u][i] = *(const d2 *)(xc[i] + r);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (!ok[u]) continue;
+      q[u][J - 1].x = invp * q[u][J - 1].x;
+      q[u][J - 1].y = invp * q[u][J - 1].y;
+      double t0 = 0.0, t1 = 0.0;
+#pragma unroll
+      for (int i = 0; i < J; ++i) {
+        t0 += q[u][i].x * P[i];
+        t1 += q[u][i].y * P[i];
       }
-    const d2 x = *(const d2 *)(xj + r);
-    const double a0 = x.x - t0, a1 = x.y - t1;
+      const double a0 = q[u][J].x - t0, a1 = q[u][J].y - t1;
 #pragma unroll
-    for (int i = 0; i < 16; ++i)
-      if (i < j) v[i] += q[i].x * a0 + q[i].y * a1;
-#pragma unroll
-    for (int i = 0; i < 17; ++i)
-      if (i == j) v[i] += a0 * a0 + a1 * a1;
+      for (int i = 0; i < J; ++i) v[i] += q[u][i].x * a0 + q[u][i].y * a1;
+      v[J] += a0 * a0 + a1 * a1;
+    }
   }
-  block_reduce_store<17>(v, j + 1, partial);
+  block_reduce_store<J + 1>(v, J + 1, partial);
 }
 
 // (ca) x1 as in (b2), x2 = x1 - sum_i X_i P2_i -> X_j (not normalised), X_{j-1} * inv[j-1]
 // -> X_{j-1}; partials [newDot_j = <x2, X_j old>, and if j + 1 < k: oldDot_{j+1},
 // <X_i, X_{j+1}> (i < j), <x2, X_{j+1}>]
-__global__ __launch_bounds__(256) void k_fb_ca(MvDesc X, int j, int has_next, const IcgsState *__restrict__ st,
-                                               int nrows, double *__restrict__ partial, int rev) {
-  double v[17];
+template <int J>
+__global__ __launch_bounds__(256) void k_fb_ca(MvDesc X, int has_next, const IcgsState *__restrict__ st, int nrows,
+                                               double *__restrict__ partial, int rev) {
+  constexpr int U = FbU<J>::U;
+  double v[J + 3];
 #pragma unroll
-  for (int i = 0; i < 17; ++i) v[i] = 0.0;
-  double P[16], P2[16];
+  for (int i = 0; i < J + 3; ++i) v[i] = 0.0;
+  double P[J], P2[J];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    P[i] = i < j ? st->P[i] : 0.0;
-    P2[i] = i < j ? st->P2[i] : 0.0;
+  for (int i = 0; i < J; ++i) {
+    P[i] = st->P[i];
+    P2[i] = st->P2[i];
   }
-  const double invp = st->inv[j - 1];
-  double *xj = colp_(X, j);
-  double *xprev = colp_(X, j - 1);
-  const double *xn = colp_(X, has_next ? j + 1 : j);
-  const long long np = (nrows + 1) / 2;
-  for (long long pp = (long long)blockIdx.x * 256 + threadIdx.x; pp < np; pp += (long long)gridDim.x * 256) {
-    const long long r = 2 * (rev ? np - 1 - pp : pp);
-    const bool two = r + 1 < nrows;
-    d2 q[16];
-    double t0 = 0.0, t1 = 0.0;
+  const double invp = st->inv[J - 1];
+  const double *xc[J + 1];
 #pragma unroll
-    for (int i = 0; i < 16; ++i)
-      if (i < j) {
-        q[i] = *(const d2 *)(colp_(X, i) + r);
-        if (i == j - 1) {
-          q[i].x = invp * q[i].x;
-          q[i].y = invp * q[i].y;
-        }
-        t0 += q[i].x * P[i];
-        t1 += q[i].y * P[i];
+  for (int i = 0; i <= J; ++i) xc[i] = colp_(X, i);
+  double *xj = colp_(X, J);
+  double *xprev = colp_(X, J - 1);
+  const double *xn = colp_(X, has_next ? J + 1 : J);
+  const long long np = (nrows + 1) / 2, stride = (long long)gridDim.x * 256;
+  for (long long p0 = (long long)blockIdx.x * 256 + threadIdx.x; p0 < np; p0 += U * stride) {
+    d2 q[U][J + 2];  // [J] = X_j old, [J + 1] = X_{j+1}
+    bool ok[U];
+    long long rr[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      rr[u] = fb_pair(p0, u, stride, np, rev, ok[u]);
+#pragma unroll
+      for (int i = 0; i <= J; ++i) q[u][i] = *(const d2 *)(xc[i] + rr[u]);
+      q[u][J + 1] = has_next ? *(const d2 *)(xn + rr[u]) : d2{0.0, 0.0};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (!ok[u]) continue;
+      const long long r = rr[u];
+      const bool two = r + 1 < nrows;
+      q[u][J - 1].x = invp * q[u][J - 1].x;
+      q[u][J - 1].y = invp * q[u][J - 1].y;
+      double t0 = 0.0, t1 = 0.0;
+#pragma unroll
+      for (int i = 0; i < J; ++i) {
+        t0 += q[u][i].x * P[i];
+        t1 += q[u][i].y * P[i];
       }
-    const d2 old = *(const d2 *)(xj + r);
-    const double s0 = old.x - t0, s1 = old.y - t1;
-    double u0 = 0.0, u1 = 0.0;
+      const d2 old = q[u][J];
+      const double s0 = old.x - t0, s1 = old.y - t1;
+      double u0 = 0.0, u1 = 0.0;
 #pragma unroll
-    for (int i = 0; i < 16; ++i)
-      if (i < j) {
-        u0 += q[i].x * P2[i];
-        u1 += q[i].y * P2[i];
+      for (int i = 0; i < J; ++i) {
+        u0 += q[u][i].x * P2[i];
+        u1 += q[u][i].y * P2[i];
       }
-    const double a0 = s0 - u0, a1 = s1 - u1;
-    v[0] += a0 * old.x + a1 * old.y;
-    st_pair(xj + r, a0, a1, two);
+      const double a0 = s0 - u0, a1 = s1 - u1;
+      v[0] += a0 * old.x + a1 * old.y;
+      st_pair(xj + r, a0, a1, two);
+      st_pair(xprev + r, q[u][J - 1].x, q[u][J - 1].y, two);
+      if (has_next) {
+        const d2 nx = q[u][J + 1];
+        v[1] += nx.x * nx.x + nx.y * nx.y;
 #pragma unroll
-    for (int i = 0; i < 16; ++i)
-      if (i == j - 1) st_pair(xprev + r, q[i].x, q[i].y, two);
-    if (has_next) {
-      const d2 nx = *(const d2 *)(xn + r);
-      v[1] += nx.x * nx.x + nx.y * nx.y;
-#pragma unroll
-      for (int i = 0; i < 16; ++i)
-        if (i < j) v[2 + i] += q[i].x * nx.x + q[i].y * nx.y;
-#pragma unroll
-      for (int i = 0; i < 16; ++i)
-        if (i == j) v[2 + i] += a0 * nx.x + a1 * nx.y;
+        for (int i = 0; i < J; ++i) v[2 + i] += q[u][i].x * nx.x + q[u][i].y * nx.y;
+        v[2 + J] += a0 * nx.x + a1 * nx.y;
+      }
     }
   }
-  block_reduce_store<17>(v, has_next ? j + 3 : 1, partial);
+  block_reduce_store<J + 3>(v, has_next ? J + 3 : 1, partial);
 }
 
 __global__ __launch_bounds__(256) void k_scale_col(MvDesc X, int j, const IcgsState *__restrict__ st, int nrows) {
@@ -1114,14 +1146,33 @@ void launch_fb_a01(hipStream_t s, MvDesc X, int nrows, double *partial, int nb) 
   k_fb_a01<<<nb, 256, 0, s>>>(X, nrows, partial);
   LAUNCH_CHECK_();
 }
+#define FB_CASES(M) M(1) M(2) M(3) M(4) M(5) M(6) M(7) M(8) M(9) M(10) M(11) M(12) M(13) M(14) M(15)
 void launch_fb_b2(hipStream_t s, MvDesc X, int j, const IcgsState *st, int nrows, double *partial, int nb,
                   int rev) {
-  k_fb_b2<<<nb, 256, 0, s>>>(X, j, st, nrows, partial, rev);
+  switch (j) {
+#define B2_CASE(J) \
+  case J:          \
+    k_fb_b2<J><<<nb, 256, 0, s>>>(X, st, nrows, partial, rev); \
+    break;
+    FB_CASES(B2_CASE)
+#undef B2_CASE
+    default:
+      throw Error(MIGMRES_EINVAL, "fb_b2: column index must be in 1..15");
+  }
   LAUNCH_CHECK_();
 }
 void launch_fb_ca(hipStream_t s, MvDesc X, int j, int has_next, const IcgsState *st, int nrows, double *partial,
                   int nb, int rev) {
-  k_fb_ca<<<nb, 256, 0, s>>>(X, j, has_next, st, nrows, partial, rev);
+  switch (j) {
+#define CA_CASE(J) \
+  case J:          \
+    k_fb_ca<J><<<nb, 256, 0, s>>>(X, has_next, st, nrows, partial, rev); \
+    break;
+    FB_CASES(CA_CASE)
+#undef CA_CASE
+    default:
+      throw Error(MIGMRES_EINVAL, "fb_ca: column index must be in 1..15");
+  }
   LAUNCH_CHECK_();
 }
 void launch_scale_col(hipStream_t s, MvDesc X, int j, const IcgsState *st, int nrows) {
