@@ -28,6 +28,8 @@ __global__ __launch_bounds__(256) void k_rw(const double *__restrict__ Q, double
       x += acc[c];
       if (MODE == 1) *(d2 *)xp = x;
       if (MODE == 2) __builtin_nontemporal_store(x, (d2 *)xp);
+      if (MODE == 3) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(xp), "v"(x) : "memory");
+      if (MODE == 4) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(xp), "v"(x) : "memory");
       if (MODE == 0 && x.x == 1234.5) out[threadIdx.x] = x.y;
     }
   }
@@ -54,15 +56,17 @@ int main() {
   CK(hipMalloc(&V, sizeof(double) * ld * 216));
   CK(hipMalloc(&o, 8192));
   CK(hipMemset(V, 0, sizeof(double) * ld * 216));
-  for (int grid : {1024, 2048, 4096}) {
+  for (int grid : {1024, 4096}) {
     for (int L : {64, 104, 200}) {
       double *X = V + (long long)L * ld;
       const double by_r = 8.0 * n * (L + k), by_rw = 8.0 * n * (L + 2 * k);
       float t0 = timeit([&] { k_rw<0, 8><<<grid, 256>>>(V, X, ld, L, n, o); });
       float t1 = timeit([&] { k_rw<1, 8><<<grid, 256>>>(V, X, ld, L, n, o); });
       float t2 = timeit([&] { k_rw<2, 8><<<grid, 256>>>(V, X, ld, L, n, o); });
-      printf("grid %4d L=%3d read-only %6.0f GB/s | plain store %6.0f GB/s | nt store %6.0f GB/s\n", grid, L,
-             by_r / t0 / 1e6, by_rw / t1 / 1e6, by_rw / t2 / 1e6);
+      float t3 = timeit([&] { k_rw<3, 8><<<grid, 256>>>(V, X, ld, L, n, o); });
+      float t4 = timeit([&] { k_rw<4, 8><<<grid, 256>>>(V, X, ld, L, n, o); });
+      printf("grid %4d L=%3d read-only %6.0f GB/s | plain store %6.0f | nt %6.0f | sc1 %6.0f | sc0 sc1 %6.0f GB/s\n", grid, L,
+             by_r / t0 / 1e6, by_rw / t1 / 1e6, by_rw / t2 / 1e6, by_rw / t3 / 1e6, by_rw / t4 / 1e6);
     }
   }
   const long long nc = n * 8 / 2;
