@@ -127,6 +127,23 @@ int migmres_crs_create_galeri(migmres_ctx *ctx, const char *kind, int nx, int ny
  * n_local+1 entries, gcols_out / vals_out *nnz_out entries). */
 int migmres_plan_galeri(const char *kind, int nx, int ny, int nz, long long first, int n_local,
                         long long *rowptr_out, long long *gcols_out, double *vals_out, long long *nnz_out);
+/* Matrix ingestion from a file (format detected from the first line):
+ *   MatrixMarket "coordinate" real/integer/pattern, general/symmetric/skew-symmetric --
+ *     replaces Tpetra::MatrixMarket::Reader<CrsMatrix>::readSparseFile
+ *     (tpetra/core/inout/MatrixMarket_Tpetra.hpp); symmetric storage expanded, duplicate
+ *     entries summed;
+ *   Harwell-Boeing RUA/RSA -- replaces Trilinos_Util_read_hb + the matrix part of
+ *     Belos::Util::createEpetraProblem (triutils/src/Trilinos_Util_read_hb.cpp,
+ *     belos/epetra/src/BelosEpetraUtils.cpp:81-160): every row carries an explicit diagonal
+ *     (MSR storage), symmetric storage expanded.
+ * crs_read_file is collective: each rank parses the file and keeps its rows of the uniform
+ * row map (Epetra_BlockMap::ConstructAutoUniform).  file_rows is the host-only form for
+ * rows [first, first+n_local), GLOBAL columns in insertion order (*nnz_out always set;
+ * arrays filled when non-NULL, as migmres_plan_galeri). */
+int migmres_matrix_file_info(const char *path, long long *n_global, long long *nnz_file, int *symmetric);
+int migmres_matrix_file_rows(const char *path, long long first, int n_local, long long *rowptr_out,
+                             long long *gcols_out, double *vals_out, long long *nnz_out);
+int migmres_crs_read_file(migmres_ctx *ctx, const char *path, migmres_crs **out);
 int migmres_crs_destroy(migmres_crs *A);
 int migmres_crs_info(const migmres_crs *A, long long *n_global, long long *first, int *n_local,
                      int *n_cols, long long *nnz_local, int *n_remote, int *n_export);

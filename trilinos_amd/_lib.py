@@ -43,6 +43,9 @@ _SIGS = {
     "migmres_crs_create": [vp, i64, i64, i32, P(i64), P(i64), P(f64), P(vp)],
     "migmres_crs_create_galeri": [vp, C.c_char_p, i32, i32, i32, P(vp)],
     "migmres_crs_destroy": [vp],
+    "migmres_matrix_file_info": [C.c_char_p, P(i64), P(i64), P(i32)],
+    "migmres_matrix_file_rows": [C.c_char_p, i64, i32, P(i64), P(i64), P(f64), P(i64)],
+    "migmres_crs_read_file": [vp, C.c_char_p, P(vp)],
     "migmres_crs_info": [vp, P(i64), P(i64), P(i32), P(i32), P(i64), P(i32), P(i32)],
     "migmres_crs_colmap": [vp, P(i64)],
     "migmres_crs_import_plan": [vp, P(i32), P(i32), P(i32), P(i32)],

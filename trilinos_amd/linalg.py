@@ -10,6 +10,7 @@ All data lives on the GPU; host arrays only cross at construction/upload/downloa
 """
 
 import ctypes as C
+import os
 
 import numpy as np
 
@@ -79,6 +80,22 @@ class Comm:
             pass
 
 
+def matrix_file_rows(path, first=0, n_local=None):
+    """Host-only read of rows [first, first + n_local) of a MatrixMarket / Harwell-Boeing file
+    (migmres_matrix_file_rows): (n_global, rowptr, global columns, values), each row's entries
+    in insertion order, duplicates summed."""
+    ng, nnz_f, sym = C.c_longlong(), C.c_longlong(), C.c_int()
+    call("migmres_matrix_file_info", os.fsencode(path), C.byref(ng), C.byref(nnz_f), C.byref(sym))
+    n_local = ng.value - first if n_local is None else n_local
+    nnz = C.c_longlong()
+    call("migmres_matrix_file_rows", os.fsencode(path), first, n_local, None, None, None, C.byref(nnz))
+    rp = np.empty(n_local + 1, dtype=np.int64)
+    gc = np.empty(max(nnz.value, 1), dtype=np.int64)
+    vv = np.empty(max(nnz.value, 1), dtype=np.float64)
+    call("migmres_matrix_file_rows", os.fsencode(path), first, n_local, lptr(rp), lptr(gc), dptr(vv), C.byref(nnz))
+    return ng.value, rp, gc[:nnz.value], vv[:nnz.value]
+
+
 class CrsMatrix:
     """Row-distributed CSR operator.  `rowptr`/`gcols`/`vals` are this rank's rows
     (uniform map) with GLOBAL column ids in insertion order; the library builds the
@@ -114,6 +131,17 @@ class CrsMatrix:
         call("migmres_crs_create_galeri", comm.h, kind.encode(), nx, ny, nz, C.byref(h))
         n = nx * ny * (nz if kind in ("Laplace3D", "Brick3D") else 1)
         return cls(comm, n, _handle=h)
+
+    @classmethod
+    def read_file(cls, comm, path):
+        """MatrixMarket / Harwell-Boeing file -> distributed operator on the uniform row map
+        (Tpetra::MatrixMarket::Reader::readSparseFile; Trilinos_Util_read_hb as used by
+        Belos::Util::createEpetraProblem).  Parsed natively on every rank."""
+        h = C.c_void_p()
+        call("migmres_crs_read_file", comm.h, os.fsencode(path), C.byref(h))
+        ng = C.c_longlong()
+        call("migmres_matrix_file_info", os.fsencode(path), C.byref(ng), None, None)
+        return cls(comm, ng.value, _handle=h)
 
     def colmap(self):
         out = np.empty(self.n_cols, dtype=np.int64)
