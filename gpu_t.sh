@@ -1,2 +1,3 @@
 source ./tools_gpu_check.sh
-step 600 pytest_gpu.log python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
+step 300 b128.json python bench.py --nx 128 --no-cpu-baseline --steps 200 --warmup 50
+step 300 b161.json python bench.py --nx 161 --no-cpu-baseline --steps 200 --warmup 50
