@@ -31,10 +31,18 @@ static inline int cdiv_(long long a, long long b) { return (int)((a + b - 1) / b
     if (e_ != hipSuccess) throw Error(MIGMRES_EHIP, std::string("kernel launch: ") + hipGetErrorString(e_)); \
   } while (0)
 
-// Fixed-order block reduction of NV values per thread -> partial[blockIdx.x * NV + i].
+// Threads per workgroup of the findBasis / closing-update passes (IC_NT = 256 or 1024; the
+// grid covers the CUs with the same number of waves either way).
+#ifndef IC_NT
+#define IC_NT 1024
+#endif
+constexpr int ICNT = IC_NT, ICNW = IC_NT / 64;
+
+// Fixed-order block reduction of NV values per thread -> partial[blockIdx.x * nv + i]:
+// wave shuffles, then a pairwise tree over the ICNW waves.
 template <int NV>
 __device__ __forceinline__ void block_reduce_store(double (&v)[NV], int nv, double *partial) {
-  __shared__ double red[4][NV];
+  __shared__ double red[ICNW][NV];
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
@@ -48,15 +56,23 @@ __device__ __forceinline__ void block_reduce_store(double (&v)[NV], int nv, doub
   __syncthreads();
   if (threadIdx.x < nv) {
     const int i = threadIdx.x;
-    partial[(long long)blockIdx.x * nv + i] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
+    double t[ICNW];
+#pragma unroll
+    for (int q = 0; q < ICNW; ++q) t[q] = red[q][i];
+#pragma unroll
+    for (int h = 1; h < ICNW; h *= 2)
+#pragma unroll
+      for (int q = 0; q + h < ICNW; q += 2 * h) t[q] = t[q] + t[q + h];
+    partial[(long long)blockIdx.x * nv + i] = t[0];
   }
 }
 
 // 1024 workgroups (4 per CU) stream the findBasis columns at 5.3-5.6 TB/s where 512 gave
 // 3.8-4.4 TB/s (tools/mb_lib.cpp, 256^3).
 int icgs_blocks(int nrows) {
-  const int b = cdiv_(nrows, 2048);
-  return b < 1 ? 1 : (b > 1024 ? 1024 : b);
+  constexpr int per = 2048 * (ICNT / 256), cap = 1024 / (ICNT / 256);
+  const int b = cdiv_(nrows, per);
+  return b < 1 ? 1 : (b > cap ? cap : b);
 }
 
 // Store rows (r, r + 1) of a column: one 16-byte store, or only row r when r + 1 == nrows
@@ -109,12 +125,12 @@ void launch_reduce_small(hipStream_t s, const double *partial, int nblocks, int 
 // of sum_r Xnew[r,c] * D[r,c] (dmode 1: D = Xnew, 2: D given).  Grid-stride over row pairs.
 // -------------------------------------------------------------------------------------
 template <int KX>
-__global__ __launch_bounds__(256) void k_gemm_nn_dot(MvDesc A, int L, const double *__restrict__ M,
+__global__ __launch_bounds__(ICNT) void k_gemm_nn_dot(MvDesc A, int L, const double *__restrict__ M,
                                                      int ldm, MvDesc X, int kx, int nrows,
                                                      double alpha, double beta, int dmode,
                                                      MvDesc D, double *__restrict__ partial) {
   extern __shared__ __attribute__((aligned(16))) double Ms[];  // L x KX
-  for (int e = threadIdx.x; e < L * KX; e += 256) {
+  for (int e = threadIdx.x; e < L * KX; e += ICNT) {
     const int j = e / KX, c = e % KX;
     Ms[e] = c < kx ? M[j + (long long)c * ldm] : 0.0;
   }
@@ -122,8 +138,8 @@ __global__ __launch_bounds__(256) void k_gemm_nn_dot(MvDesc A, int L, const doub
   double dacc[KX + 1];  // dmode 3: [KX] = <Xnew_0, Xnew_1> (findBasis head, see k_fb_scalar stage 7)
 #pragma unroll
   for (int c = 0; c <= KX; ++c) dacc[c] = 0.0;
-  for (long long r = 2LL * ((long long)blockIdx.x * 256 + threadIdx.x); r < nrows;
-       r += 2LL * gridDim.x * 256) {
+  for (long long r = 2LL * ((long long)blockIdx.x * ICNT + threadIdx.x); r < nrows;
+       r += 2LL * gridDim.x * ICNT) {
     const bool two = r + 1 < nrows;
     double acc0[KX], acc1[KX];
 #pragma unroll
@@ -210,11 +226,11 @@ void launch_gemm_nn_dot(hipStream_t s, MvDesc A, int L, const double *M, int ldm
   const int KX = kx <= 1 ? 1 : kx <= 2 ? 2 : kx <= 4 ? 4 : kx <= 8 ? 8 : 16;
   const size_t lds = sizeof(double) * (size_t)(L > 0 ? L : 1) * KX;
   switch (KX) {
-    case 1: k_gemm_nn_dot<1><<<nblocks, 256, lds, s>>>(A, L, M, ldm, X, kx, nrows, alpha, beta, dmode, D, partial); break;
-    case 2: k_gemm_nn_dot<2><<<nblocks, 256, lds, s>>>(A, L, M, ldm, X, kx, nrows, alpha, beta, dmode, D, partial); break;
-    case 4: k_gemm_nn_dot<4><<<nblocks, 256, lds, s>>>(A, L, M, ldm, X, kx, nrows, alpha, beta, dmode, D, partial); break;
-    case 8: k_gemm_nn_dot<8><<<nblocks, 256, lds, s>>>(A, L, M, ldm, X, kx, nrows, alpha, beta, dmode, D, partial); break;
-    default: k_gemm_nn_dot<16><<<nblocks, 256, lds, s>>>(A, L, M, ldm, X, kx, nrows, alpha, beta, dmode, D, partial); break;
+    case 1: k_gemm_nn_dot<1><<<nblocks, ICNT, lds, s>>>(A, L, M, ldm, X, kx, nrows, alpha, beta, dmode, D, partial); break;
+    case 2: k_gemm_nn_dot<2><<<nblocks, ICNT, lds, s>>>(A, L, M, ldm, X, kx, nrows, alpha, beta, dmode, D, partial); break;
+    case 4: k_gemm_nn_dot<4><<<nblocks, ICNT, lds, s>>>(A, L, M, ldm, X, kx, nrows, alpha, beta, dmode, D, partial); break;
+    case 8: k_gemm_nn_dot<8><<<nblocks, ICNT, lds, s>>>(A, L, M, ldm, X, kx, nrows, alpha, beta, dmode, D, partial); break;
+    default: k_gemm_nn_dot<16><<<nblocks, ICNT, lds, s>>>(A, L, M, ldm, X, kx, nrows, alpha, beta, dmode, D, partial); break;
   }
   LAUNCH_CHECK_();
 }
@@ -689,7 +705,7 @@ void launch_nn_tn(hipStream_t s, MvDesc Q, int L, const double *C1, int ldc, MvD
 // Row pairs: each thread handles rows (r, r+1) with 16-byte loads; the padding row of a
 // pair (r+1 == nrows) reads the zero padding and is never written.
 // (a) normalise column j-1 in place by inv[j-1]; partials [oldDot_j, <X_i, X_j> i<j]
-__global__ __launch_bounds__(256) void k_fb_a(MvDesc X, int j, const IcgsState *__restrict__ st,
+__global__ __launch_bounds__(ICNT) void k_fb_a(MvDesc X, int j, const IcgsState *__restrict__ st,
                                               int nrows, double *__restrict__ partial) {
   double v[17];
 #pragma unroll
@@ -697,8 +713,8 @@ __global__ __launch_bounds__(256) void k_fb_a(MvDesc X, int j, const IcgsState *
   const double invp = j > 0 ? st->inv[j - 1] : 1.0;
   double *xj = colp_(X, j);
   double *xp = j > 0 ? colp_(X, j - 1) : xj;
-  for (long long r = 2LL * ((long long)blockIdx.x * 256 + threadIdx.x); r < nrows;
-       r += 2LL * gridDim.x * 256) {
+  for (long long r = 2LL * ((long long)blockIdx.x * ICNT + threadIdx.x); r < nrows;
+       r += 2LL * gridDim.x * ICNT) {
     const d2 x = *(const d2 *)(xj + r);
     v[0] += x.x * x.x + x.y * x.y;
     if (j > 0) {
@@ -720,7 +736,7 @@ __global__ __launch_bounds__(256) void k_fb_a(MvDesc X, int j, const IcgsState *
 }
 
 // (b) x1 = X_j - sum_i X_i P_i  -> S ; partials <X_i, x1> (i < j)
-__global__ __launch_bounds__(256) void k_fb_b(MvDesc X, int j, const IcgsState *__restrict__ st,
+__global__ __launch_bounds__(ICNT) void k_fb_b(MvDesc X, int j, const IcgsState *__restrict__ st,
                                               double *__restrict__ S, int nrows,
                                               double *__restrict__ partial) {
   double v[16];
@@ -731,8 +747,8 @@ __global__ __launch_bounds__(256) void k_fb_b(MvDesc X, int j, const IcgsState *
     P[i] = i < j ? st->P[i] : 0.0;
   }
   const double *xj = colp_(X, j);
-  for (long long r = 2LL * ((long long)blockIdx.x * 256 + threadIdx.x); r < nrows;
-       r += 2LL * gridDim.x * 256) {
+  for (long long r = 2LL * ((long long)blockIdx.x * ICNT + threadIdx.x); r < nrows;
+       r += 2LL * gridDim.x * ICNT) {
     d2 q[16];
     double t0 = 0.0, t1 = 0.0;
 #pragma unroll
@@ -753,7 +769,7 @@ __global__ __launch_bounds__(256) void k_fb_b(MvDesc X, int j, const IcgsState *
 }
 
 // (c) x2 = S - sum_i X_i P2_i -> X_j ; partials <x2, X_j(old)>
-__global__ __launch_bounds__(256) void k_fb_c(MvDesc X, int j, const IcgsState *__restrict__ st,
+__global__ __launch_bounds__(ICNT) void k_fb_c(MvDesc X, int j, const IcgsState *__restrict__ st,
                                               const double *__restrict__ S, int nrows,
                                               double *__restrict__ partial) {
   double v[1] = {0.0};
@@ -761,8 +777,8 @@ __global__ __launch_bounds__(256) void k_fb_c(MvDesc X, int j, const IcgsState *
 #pragma unroll
   for (int i = 0; i < 16; ++i) P[i] = i < j ? st->P2[i] : 0.0;
   double *xj = colp_(X, j);
-  for (long long r = 2LL * ((long long)blockIdx.x * 256 + threadIdx.x); r < nrows;
-       r += 2LL * gridDim.x * 256) {
+  for (long long r = 2LL * ((long long)blockIdx.x * ICNT + threadIdx.x); r < nrows;
+       r += 2LL * gridDim.x * ICNT) {
     double t0 = 0.0, t1 = 0.0;
 #pragma unroll
     for (int i = 0; i < 16; ++i)
@@ -791,11 +807,11 @@ __global__ __launch_bounds__(256) void k_fb_c(MvDesc X, int j, const IcgsState *
 // column per step; k_fb_b2 is read-only.
 //
 // (a01) partials [oldDot_0, oldDot_1, <X_0, X_1>] with X_0 not yet normalised.
-__global__ __launch_bounds__(256) void k_fb_a01(MvDesc X, int nrows, double *__restrict__ partial) {
+__global__ __launch_bounds__(ICNT) void k_fb_a01(MvDesc X, int nrows, double *__restrict__ partial) {
   double v[3] = {0.0, 0.0, 0.0};
   const double *x0 = colp_(X, 0), *x1 = colp_(X, 1);
-  for (long long r = 2LL * ((long long)blockIdx.x * 256 + threadIdx.x); r < nrows;
-       r += 2LL * gridDim.x * 256) {
+  for (long long r = 2LL * ((long long)blockIdx.x * ICNT + threadIdx.x); r < nrows;
+       r += 2LL * gridDim.x * ICNT) {
     const d2 a = *(const d2 *)(x0 + r);
     const d2 b = *(const d2 *)(x1 + r);
     v[0] += a.x * a.x + a.y * a.y;
@@ -828,7 +844,7 @@ __device__ __forceinline__ long long fb_pair(long long p0, int u, long long stri
 // (b2) x1 = X_j - sum_i X_i P_i with X_{j-1} scaled by inv[j-1]; partials <X_i, x1> (i < j)
 // and <x1, x1> (index j, the DGKS re-orthogonalisation test).  Writes nothing.
 template <int J>
-__global__ __launch_bounds__(256) void k_fb_b2(MvDesc X, const IcgsState *__restrict__ st, int nrows,
+__global__ __launch_bounds__(ICNT) void k_fb_b2(MvDesc X, const IcgsState *__restrict__ st, int nrows,
                                                double *__restrict__ partial, int rev) {
   constexpr int U = FbU<J>::U;
   double v[J + 1];
@@ -841,8 +857,8 @@ __global__ __launch_bounds__(256) void k_fb_b2(MvDesc X, const IcgsState *__rest
   const double *xc[J + 1];
 #pragma unroll
   for (int i = 0; i <= J; ++i) xc[i] = colp_(X, i);
-  const long long np = (nrows + 1) / 2, stride = (long long)gridDim.x * 256;
-  for (long long p0 = (long long)blockIdx.x * 256 + threadIdx.x; p0 < np; p0 += U * stride) {
+  const long long np = (nrows + 1) / 2, stride = (long long)gridDim.x * ICNT;
+  for (long long p0 = (long long)blockIdx.x * ICNT + threadIdx.x; p0 < np; p0 += U * stride) {
     d2 q[U][J + 1];
     bool ok[U];
 #pragma unroll
@@ -875,7 +891,7 @@ __global__ __launch_bounds__(256) void k_fb_b2(MvDesc X, const IcgsState *__rest
 // -> X_{j-1}; partials [newDot_j = <x2, X_j old>, and if j + 1 < k: oldDot_{j+1},
 // <X_i, X_{j+1}> (i < j), <x2, X_{j+1}>]
 template <int J>
-__global__ __launch_bounds__(256) void k_fb_ca(MvDesc X, int has_next, const IcgsState *__restrict__ st, int nrows,
+__global__ __launch_bounds__(ICNT) void k_fb_ca(MvDesc X, int has_next, const IcgsState *__restrict__ st, int nrows,
                                                double *__restrict__ partial, int rev) {
   constexpr int U = FbU<J>::U;
   double v[J + 3];
@@ -894,8 +910,8 @@ __global__ __launch_bounds__(256) void k_fb_ca(MvDesc X, int has_next, const Icg
   double *xj = colp_(X, J);
   double *xprev = colp_(X, J - 1);
   const double *xn = colp_(X, has_next ? J + 1 : J);
-  const long long np = (nrows + 1) / 2, stride = (long long)gridDim.x * 256;
-  for (long long p0 = (long long)blockIdx.x * 256 + threadIdx.x; p0 < np; p0 += U * stride) {
+  const long long np = (nrows + 1) / 2, stride = (long long)gridDim.x * ICNT;
+  for (long long p0 = (long long)blockIdx.x * ICNT + threadIdx.x; p0 < np; p0 += U * stride) {
     d2 q[U][J + 2];  // [J] = X_j old, [J + 1] = X_{j+1}
     bool ok[U];
     long long rr[U];
@@ -1130,20 +1146,20 @@ __global__ void k_add_coef(const double *__restrict__ C1, int ld1, const double 
 }
 
 void launch_fb_a(hipStream_t s, MvDesc X, int j, const IcgsState *st, int nrows, double *partial, int nb) {
-  k_fb_a<<<nb, 256, 0, s>>>(X, j, st, nrows, partial);
+  k_fb_a<<<nb, ICNT, 0, s>>>(X, j, st, nrows, partial);
   LAUNCH_CHECK_();
 }
 void launch_fb_b(hipStream_t s, MvDesc X, int j, const IcgsState *st, double *S, int nrows, double *partial, int nb) {
-  k_fb_b<<<nb, 256, 0, s>>>(X, j, st, S, nrows, partial);
+  k_fb_b<<<nb, ICNT, 0, s>>>(X, j, st, S, nrows, partial);
   LAUNCH_CHECK_();
 }
 void launch_fb_c(hipStream_t s, MvDesc X, int j, const IcgsState *st, const double *S, int nrows, double *partial,
                  int nb) {
-  k_fb_c<<<nb, 256, 0, s>>>(X, j, st, S, nrows, partial);
+  k_fb_c<<<nb, ICNT, 0, s>>>(X, j, st, S, nrows, partial);
   LAUNCH_CHECK_();
 }
 void launch_fb_a01(hipStream_t s, MvDesc X, int nrows, double *partial, int nb) {
-  k_fb_a01<<<nb, 256, 0, s>>>(X, nrows, partial);
+  k_fb_a01<<<nb, ICNT, 0, s>>>(X, nrows, partial);
   LAUNCH_CHECK_();
 }
 #define FB_CASES(M) M(1) M(2) M(3) M(4) M(5) M(6) M(7) M(8) M(9) M(10) M(11) M(12) M(13) M(14) M(15)
@@ -1152,7 +1168,7 @@ void launch_fb_b2(hipStream_t s, MvDesc X, int j, const IcgsState *st, int nrows
   switch (j) {
 #define B2_CASE(J) \
   case J:          \
-    k_fb_b2<J><<<nb, 256, 0, s>>>(X, st, nrows, partial, rev); \
+    k_fb_b2<J><<<nb, ICNT, 0, s>>>(X, st, nrows, partial, rev); \
     break;
     FB_CASES(B2_CASE)
 #undef B2_CASE
@@ -1166,7 +1182,7 @@ void launch_fb_ca(hipStream_t s, MvDesc X, int j, int has_next, const IcgsState 
   switch (j) {
 #define CA_CASE(J) \
   case J:          \
-    k_fb_ca<J><<<nb, 256, 0, s>>>(X, has_next, st, nrows, partial, rev); \
+    k_fb_ca<J><<<nb, ICNT, 0, s>>>(X, has_next, st, nrows, partial, rev); \
     break;
     FB_CASES(CA_CASE)
 #undef CA_CASE
