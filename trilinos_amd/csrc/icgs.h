@@ -17,6 +17,22 @@ struct IcgsState {
   double dep_tol;
 };
 
+// Pass prologue: the reduction + scalar step still pending from the previous pass, taken by
+// every workgroup of the next pass from the previous pass's per-workgroup partials (one
+// rank) or from the all-reduced vector (several ranks), instead of a separate launch.
+// Every workgroup applies the step to its own LDS copy of `in`; workgroup 0 also stores the
+// result to `out` (the state double-buffers: the other workgroups still read `in`).
+// stage0 < 0: nothing pending (`in` is used as is, `out` unused).
+struct FbPro {
+  const double *partial;  // partial[b * nv + i], b < nblocks; nullptr: use red
+  const double *red;
+  int nblocks, nv;
+  int stage0, stage1;  // scalar stages applied in order (stage1 < 0: only stage0)
+  int j, k, complete;
+  const IcgsState *in;
+  IcgsState *out;
+};
+
 int icgs_blocks(int nrows);
 void launch_reduce_small(hipStream_t s, const double *partial, int nblocks, int nv, double *out);
 void launch_gemm_nn_dot(hipStream_t s, MvDesc A, int L, const double *M, int ldm, MvDesc X,
@@ -30,7 +46,7 @@ bool nn_tn_supported(int L, int k);
 int nn_tn_blocks(int nrows, int L, int k);
 void launch_nn_tn(hipStream_t s, MvDesc Q, int L, const double *C1, int ldc, MvDesc X, int nrows,
                   double *partial, int nblocks, double *sink, bool store_x1 = true);
-void launch_fb_a(hipStream_t s, MvDesc X, int j, const IcgsState *st, int nrows, double *partial, int nb);
+void launch_fb_a(hipStream_t s, MvDesc X, int j, const FbPro &pro, int nrows, double *partial, int nb);
 void launch_fb_b(hipStream_t s, MvDesc X, int j, const IcgsState *st, double *S, int nrows, double *partial, int nb);
 void launch_fb_c(hipStream_t s, MvDesc X, int j, const IcgsState *st, const double *S, int nrows, double *partial,
                  int nb);
@@ -39,11 +55,13 @@ void launch_fb_c(hipStream_t s, MvDesc X, int j, const IcgsState *st, const doub
 // rev = 1 sweeps the rows from the top down: consecutive passes alternate direction so each
 // pass starts on the rows the previous one touched last (still in the Infinity Cache).
 void launch_fb_a01(hipStream_t s, MvDesc X, int nrows, double *partial, int nb);
-void launch_fb_b2(hipStream_t s, MvDesc X, int j, const IcgsState *st, int nrows, double *partial, int nb,
+void launch_fb_b2(hipStream_t s, MvDesc X, int j, const FbPro &pro, int nrows, double *partial, int nb,
                   int rev = 0);
-void launch_fb_ca(hipStream_t s, MvDesc X, int j, int has_next, const IcgsState *st, int nrows, double *partial,
+void launch_fb_ca(hipStream_t s, MvDesc X, int j, int has_next, const FbPro &pro, int nrows, double *partial,
                   int nb, int rev = 0);
-void launch_scale_col(hipStream_t s, MvDesc X, int j, const IcgsState *st, int nrows);
+void launch_scale_col(hipStream_t s, MvDesc X, int j, const FbPro &pro, int nrows, int nb);
+// the prologue alone (one workgroup): applies a pending step with nothing after it
+void launch_fb_flush(hipStream_t s, const FbPro &pro);
 // reduce_small followed by fb_scalar in one single-workgroup launch (single rank only)
 void launch_reduce_scalar(hipStream_t s, const double *partial, int nblocks, int nv, double *red, IcgsState *st,
                           int stage, int j, int k, int complete);

@@ -38,6 +38,17 @@ static inline int cdiv_(long long a, long long b) { return (int)((a + b - 1) / b
 #endif
 constexpr int ICNT = IC_NT, ICNW = IC_NT / 64;
 
+// Row b of per-workgroup partials (nv <= 17 values) added into v: all 17 loads issued
+// unconditionally (indices clamped into the row, values past nv dropped by a select), so
+// they are in flight together -- a branch per value made each load wait for the previous.
+__device__ __forceinline__ void add_partial_row(double (&v)[17], const double *partial, long long b, int nv) {
+  double x[17];
+#pragma unroll
+  for (int i = 0; i < 17; ++i) x[i] = partial[b * nv + (i < nv ? i : nv - 1)];
+#pragma unroll
+  for (int i = 0; i < 17; ++i) v[i] += i < nv ? x[i] : 0.0;
+}
+
 // Fixed-order block reduction of NV values per thread -> partial[blockIdx.x * nv + i]:
 // wave shuffles, then a pairwise tree over the ICNW waves.
 template <int NV>
@@ -67,6 +78,68 @@ __device__ __forceinline__ void block_reduce_store(double (&v)[NV], int nv, doub
   }
 }
 
+__device__ void fb_scalar_body(IcgsState *st, const double *red, int stage, int j, int k, int complete);
+
+// The pass prologue (FbPro, icgs.h): every workgroup copies the state into LDS, reduces the
+// previous pass's partials in a fixed order (the same bits in every workgroup: same data,
+// same code) and applies the pending scalar step(s) to its copy; workgroup 0 stores the
+// result.  The partials are at most 256 rows x 17 values (35 KB, served from L2 to all but
+// the first readers).
+__device__ void fb_prologue(const FbPro &p, IcgsState *ls) {
+  __shared__ double redv[17];
+  __shared__ double wred[ICNW][17];
+  constexpr int NWORD = sizeof(IcgsState) / 8;
+  static_assert(sizeof(IcgsState) % 8 == 0, "IcgsState is copied in 8-byte words");
+  for (int e = threadIdx.x; e < NWORD; e += blockDim.x) ((long long *)ls)[e] = ((const long long *)p.in)[e];
+  if (p.stage0 >= 0) {
+    if (p.partial) {
+      double v[17];
+#pragma unroll
+      for (int i = 0; i < 17; ++i) v[i] = 0.0;
+      for (int b = threadIdx.x; b < p.nblocks; b += blockDim.x) {
+        add_partial_row(v, p.partial, b, p.nv);
+      }
+      const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+      for (int i = 0; i < 17; ++i) {
+        if (i < p.nv) {
+          double x = v[i];
+#pragma unroll
+          for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off, 64);
+          if (l == 0) wred[w][i] = x;
+        }
+      }
+      __syncthreads();
+      if (threadIdx.x < p.nv) {
+        const int i = threadIdx.x;
+        double t[ICNW];
+#pragma unroll
+        for (int q = 0; q < ICNW; ++q) t[q] = wred[q][i];
+#pragma unroll
+        for (int h = 1; h < ICNW; h *= 2)
+#pragma unroll
+          for (int q = 0; q + h < ICNW; q += 2 * h) t[q] = t[q] + t[q + h];
+        redv[i] = t[0];
+      }
+    } else if (threadIdx.x < p.nv) {
+      redv[threadIdx.x] = p.red[threadIdx.x];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      fb_scalar_body(ls, redv, p.stage0, p.j, p.k, p.complete);
+      if (p.stage1 >= 0) fb_scalar_body(ls, redv, p.stage1, p.j, p.k, p.complete);
+    }
+  }
+  __syncthreads();
+  if (p.stage0 >= 0 && p.out && blockIdx.x == 0)
+    for (int e = threadIdx.x; e < NWORD; e += blockDim.x) ((long long *)p.out)[e] = ((const long long *)ls)[e];
+}
+
+__global__ __launch_bounds__(ICNT) void k_fb_flush(FbPro pro) {
+  __shared__ IcgsState ls;
+  fb_prologue(pro, &ls);
+}
+
 // 1024 workgroups (4 per CU) stream the findBasis columns at 5.3-5.6 TB/s where 512 gave
 // 3.8-4.4 TB/s (tools/mb_lib.cpp, 256^3).
 int icgs_blocks(int nrows) {
@@ -93,9 +166,7 @@ __global__ __launch_bounds__(256) void k_reduce_small(const double *__restrict__
 #pragma unroll
   for (int i = 0; i < 17; ++i) v[i] = 0.0;
   for (int b = threadIdx.x; b < nblocks; b += 256) {
-#pragma unroll
-    for (int i = 0; i < 17; ++i)
-      if (i < nv) v[i] += partial[(long long)b * nv + i];
+    add_partial_row(v, partial, b, nv);
   }
   __shared__ double red[4][17];
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -271,6 +342,75 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
+}
+
+// The prologue split in two so that a pass can issue its first row loads in between:
+// fb_pro_load issues this thread's global loads (one state word, its rows of partials);
+// fb_pro_finish consumes them with LDS traffic and raw barriers only, so the pass's loads
+// issued in between stay in flight (a __syncthreads() would wait for them: vmcnt(0)).
+struct ProRegs {
+  long long w;
+  double v[17];
+};
+
+__device__ __forceinline__ void fb_pro_load(const FbPro &p, ProRegs &r) {
+  constexpr int NWORD = sizeof(IcgsState) / 8;
+  static_assert(NWORD <= ICNT, "one state word per thread");
+  const int t = threadIdx.x;
+  r.w = t < NWORD ? ((const long long *)p.in)[t] : 0;
+#pragma unroll
+  for (int i = 0; i < 17; ++i) r.v[i] = 0.0;
+  if (p.stage0 >= 0) {
+    if (p.partial) {
+      for (int b = t; b < p.nblocks; b += ICNT) {
+        add_partial_row(r.v, p.partial, b, p.nv);
+      }
+    } else if (t < p.nv) {
+      r.v[0] = p.red[t];
+    }
+  }
+}
+
+__device__ __forceinline__ void fb_pro_finish(const FbPro &p, ProRegs &r, IcgsState *ls) {
+  __shared__ double redv[17];
+  __shared__ double wred[ICNW][17];
+  constexpr int NWORD = sizeof(IcgsState) / 8;
+  const int t = threadIdx.x;
+  if (t < NWORD) ((long long *)ls)[t] = r.w;
+  if (p.stage0 >= 0) {
+    if (p.partial) {
+      const int l = t & 63, w = t >> 6;
+#pragma unroll
+      for (int i = 0; i < 17; ++i) {
+        if (i < p.nv) {
+          double x = r.v[i];
+#pragma unroll
+          for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off, 64);
+          if (l == 0) wred[w][i] = x;
+        }
+      }
+      lds_barrier();
+      if (t < p.nv) {
+        double q[ICNW];
+#pragma unroll
+        for (int w2 = 0; w2 < ICNW; ++w2) q[w2] = wred[w2][t];
+#pragma unroll
+        for (int h = 1; h < ICNW; h *= 2)
+#pragma unroll
+          for (int w2 = 0; w2 + h < ICNW; w2 += 2 * h) q[w2] = q[w2] + q[w2 + h];
+        redv[t] = q[0];
+      }
+    } else if (t < p.nv) {
+      redv[t] = r.v[0];
+    }
+    lds_barrier();
+    if (t == 0) {
+      fb_scalar_body(ls, redv, p.stage0, p.j, p.k, p.complete);
+      if (p.stage1 >= 0) fb_scalar_body(ls, redv, p.stage1, p.j, p.k, p.complete);
+    }
+  }
+  lds_barrier();
+  if (p.stage0 >= 0 && p.out && blockIdx.x == 0 && t < NWORD) ((long long *)p.out)[t] = ((const long long *)ls)[t];
 }
 
 __device__ __forceinline__ double mfma4(double a, double b, double c) {
@@ -705,12 +845,14 @@ void launch_nn_tn(hipStream_t s, MvDesc Q, int L, const double *C1, int ldc, MvD
 // Row pairs: each thread handles rows (r, r+1) with 16-byte loads; the padding row of a
 // pair (r+1 == nrows) reads the zero padding and is never written.
 // (a) normalise column j-1 in place by inv[j-1]; partials [oldDot_j, <X_i, X_j> i<j]
-__global__ __launch_bounds__(ICNT) void k_fb_a(MvDesc X, int j, const IcgsState *__restrict__ st,
-                                              int nrows, double *__restrict__ partial) {
+__global__ __launch_bounds__(ICNT) void k_fb_a(MvDesc X, int j, FbPro pro, int nrows,
+                                              double *__restrict__ partial) {
+  __shared__ IcgsState ls;
+  fb_prologue(pro, &ls);
   double v[17];
 #pragma unroll
   for (int i = 0; i < 17; ++i) v[i] = 0.0;
-  const double invp = j > 0 ? st->inv[j - 1] : 1.0;
+  const double invp = j > 0 ? ls.inv[j - 1] : 1.0;
   double *xj = colp_(X, j);
   double *xp = j > 0 ? colp_(X, j - 1) : xj;
   for (long long r = 2LL * ((long long)blockIdx.x * ICNT + threadIdx.x); r < nrows;
@@ -844,29 +986,38 @@ __device__ __forceinline__ long long fb_pair(long long p0, int u, long long stri
 // (b2) x1 = X_j - sum_i X_i P_i with X_{j-1} scaled by inv[j-1]; partials <X_i, x1> (i < j)
 // and <x1, x1> (index j, the DGKS re-orthogonalisation test).  Writes nothing.
 template <int J>
-__global__ __launch_bounds__(ICNT) void k_fb_b2(MvDesc X, const IcgsState *__restrict__ st, int nrows,
-                                               double *__restrict__ partial, int rev) {
+__global__ __launch_bounds__(ICNT) void k_fb_b2(MvDesc X, FbPro pro, int nrows, double *__restrict__ partial,
+                                               int rev) {
   constexpr int U = FbU<J>::U;
-  double v[J + 1];
-  double P[J];
-#pragma unroll
-  for (int i = 0; i <= J; ++i) v[i] = 0.0;
-#pragma unroll
-  for (int i = 0; i < J; ++i) P[i] = st->P[i];
-  const double invp = st->inv[J - 1];
+  ProRegs pr;
+  fb_pro_load(pro, pr);
   const double *xc[J + 1];
 #pragma unroll
   for (int i = 0; i <= J; ++i) xc[i] = colp_(X, i);
   const long long np = (nrows + 1) / 2, stride = (long long)gridDim.x * ICNT;
-  for (long long p0 = (long long)blockIdx.x * ICNT + threadIdx.x; p0 < np; p0 += U * stride) {
-    d2 q[U][J + 1];
-    bool ok[U];
+  d2 q[U][J + 1];
+  bool ok[U];
+  // rows of group p0 (clamped past the end: loaded, not used)
+  auto load = [&](long long p0) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const long long r = fb_pair(p0, u, stride, np, rev, ok[u]);
 #pragma unroll
       for (int i = 0; i <= J; ++i) q[u][i] = *(const d2 *)(xc[i] + r);
     }
+  };
+  long long p0 = (long long)blockIdx.x * ICNT + threadIdx.x;
+  load(p0);  // in flight during the prologue
+  __shared__ IcgsState ls;
+  fb_pro_finish(pro, pr, &ls);
+  double v[J + 1];
+  double P[J];
+#pragma unroll
+  for (int i = 0; i <= J; ++i) v[i] = 0.0;
+#pragma unroll
+  for (int i = 0; i < J; ++i) P[i] = ls.P[i];
+  const double invp = ls.inv[J - 1];
+  for (; p0 < np; p0 += U * stride) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if (!ok[u]) continue;
@@ -883,6 +1034,7 @@ __global__ __launch_bounds__(ICNT) void k_fb_b2(MvDesc X, const IcgsState *__res
       for (int i = 0; i < J; ++i) v[i] += q[u][i].x * a0 + q[u][i].y * a1;
       v[J] += a0 * a0 + a1 * a1;
     }
+    load(p0 + U * stride);
   }
   block_reduce_store<J + 1>(v, J + 1, partial);
 }
@@ -891,19 +1043,11 @@ __global__ __launch_bounds__(ICNT) void k_fb_b2(MvDesc X, const IcgsState *__res
 // -> X_{j-1}; partials [newDot_j = <x2, X_j old>, and if j + 1 < k: oldDot_{j+1},
 // <X_i, X_{j+1}> (i < j), <x2, X_{j+1}>]
 template <int J>
-__global__ __launch_bounds__(ICNT) void k_fb_ca(MvDesc X, int has_next, const IcgsState *__restrict__ st, int nrows,
+__global__ __launch_bounds__(ICNT) void k_fb_ca(MvDesc X, int has_next, FbPro pro, int nrows,
                                                double *__restrict__ partial, int rev) {
   constexpr int U = FbU<J>::U;
-  double v[J + 3];
-#pragma unroll
-  for (int i = 0; i < J + 3; ++i) v[i] = 0.0;
-  double P[J], P2[J];
-#pragma unroll
-  for (int i = 0; i < J; ++i) {
-    P[i] = st->P[i];
-    P2[i] = st->P2[i];
-  }
-  const double invp = st->inv[J - 1];
+  ProRegs pr;
+  fb_pro_load(pro, pr);
   const double *xc[J + 1];
 #pragma unroll
   for (int i = 0; i <= J; ++i) xc[i] = colp_(X, i);
@@ -911,10 +1055,10 @@ __global__ __launch_bounds__(ICNT) void k_fb_ca(MvDesc X, int has_next, const Ic
   double *xprev = colp_(X, J - 1);
   const double *xn = colp_(X, has_next ? J + 1 : J);
   const long long np = (nrows + 1) / 2, stride = (long long)gridDim.x * ICNT;
-  for (long long p0 = (long long)blockIdx.x * ICNT + threadIdx.x; p0 < np; p0 += U * stride) {
-    d2 q[U][J + 2];  // [J] = X_j old, [J + 1] = X_{j+1}
-    bool ok[U];
-    long long rr[U];
+  d2 q[U][J + 2];  // [J] = X_j old, [J + 1] = X_{j+1}
+  bool ok[U];
+  long long rr[U];
+  auto load = [&](long long p0) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       rr[u] = fb_pair(p0, u, stride, np, rev, ok[u]);
@@ -922,6 +1066,22 @@ __global__ __launch_bounds__(ICNT) void k_fb_ca(MvDesc X, int has_next, const Ic
       for (int i = 0; i <= J; ++i) q[u][i] = *(const d2 *)(xc[i] + rr[u]);
       q[u][J + 1] = has_next ? *(const d2 *)(xn + rr[u]) : d2{0.0, 0.0};
     }
+  };
+  long long p0 = (long long)blockIdx.x * ICNT + threadIdx.x;
+  load(p0);  // in flight during the prologue
+  __shared__ IcgsState ls;
+  fb_pro_finish(pro, pr, &ls);
+  double v[J + 3];
+#pragma unroll
+  for (int i = 0; i < J + 3; ++i) v[i] = 0.0;
+  double P[J], P2[J];
+#pragma unroll
+  for (int i = 0; i < J; ++i) {
+    P[i] = ls.P[i];
+    P2[i] = ls.P2[i];
+  }
+  const double invp = ls.inv[J - 1];
+  for (; p0 < np; p0 += U * stride) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if (!ok[u]) continue;
@@ -955,22 +1115,27 @@ __global__ __launch_bounds__(ICNT) void k_fb_ca(MvDesc X, int has_next, const Ic
         v[2 + J] += a0 * nx.x + a1 * nx.y;
       }
     }
+    load(p0 + U * stride);
   }
   block_reduce_store<J + 3>(v, has_next ? J + 3 : 1, partial);
 }
 
-__global__ __launch_bounds__(256) void k_scale_col(MvDesc X, int j, const IcgsState *__restrict__ st, int nrows) {
-  const long long r = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (r < nrows) {
-    double *p = colp_(X, j) + r;
-    *p = st->inv[j] * (*p);
+__global__ __launch_bounds__(ICNT) void k_scale_col(MvDesc X, int j, FbPro pro, int nrows) {
+  __shared__ IcgsState ls;
+  fb_prologue(pro, &ls);
+  const double inv = ls.inv[j];
+  double *x = colp_(X, j);
+  const long long np = (nrows + 1) / 2;
+  for (long long pp = (long long)blockIdx.x * ICNT + threadIdx.x; pp < np; pp += (long long)gridDim.x * ICNT) {
+    const long long r = 2 * pp;
+    const d2 v = *(const d2 *)(x + r);
+    st_pair(x + r, inv * v.x, inv * v.y, r + 1 < nrows);
   }
 }
 
 // Scalar step after a reduction (red = reduced vector).  stage: 0 after (a), 1 after (b),
 // 2 after (c), 3 after blkOrtho's projections (C = C1 + C2, dependency test), 4 for the
 // k == 1 normalisation.
-__device__ void fb_scalar_body(IcgsState *st, const double *red, int stage, int j, int k, int complete);
 
 __global__ void k_fb_scalar(IcgsState *st, const double *__restrict__ red, int stage, int j, int k,
                             int complete) {
@@ -987,9 +1152,7 @@ __global__ __launch_bounds__(256) void k_reduce_scalar(const double *__restrict_
 #pragma unroll
   for (int i = 0; i < 17; ++i) v[i] = 0.0;
   for (int b = threadIdx.x; b < nblocks; b += 256) {
-#pragma unroll
-    for (int i = 0; i < 17; ++i)
-      if (i < nv) v[i] += partial[(long long)b * nv + i];
+    add_partial_row(v, partial, b, nv);
   }
   __shared__ double red[4][17];
   __shared__ double sum[17];
@@ -1145,8 +1308,8 @@ __global__ void k_add_coef(const double *__restrict__ C1, int ld1, const double 
   out[i + (long long)j * ldo] = C1[i + (long long)j * ld1] + C2[i + (long long)j * ld2];
 }
 
-void launch_fb_a(hipStream_t s, MvDesc X, int j, const IcgsState *st, int nrows, double *partial, int nb) {
-  k_fb_a<<<nb, ICNT, 0, s>>>(X, j, st, nrows, partial);
+void launch_fb_a(hipStream_t s, MvDesc X, int j, const FbPro &pro, int nrows, double *partial, int nb) {
+  k_fb_a<<<nb, ICNT, 0, s>>>(X, j, pro, nrows, partial);
   LAUNCH_CHECK_();
 }
 void launch_fb_b(hipStream_t s, MvDesc X, int j, const IcgsState *st, double *S, int nrows, double *partial, int nb) {
@@ -1163,12 +1326,12 @@ void launch_fb_a01(hipStream_t s, MvDesc X, int nrows, double *partial, int nb) 
   LAUNCH_CHECK_();
 }
 #define FB_CASES(M) M(1) M(2) M(3) M(4) M(5) M(6) M(7) M(8) M(9) M(10) M(11) M(12) M(13) M(14) M(15)
-void launch_fb_b2(hipStream_t s, MvDesc X, int j, const IcgsState *st, int nrows, double *partial, int nb,
+void launch_fb_b2(hipStream_t s, MvDesc X, int j, const FbPro &pro, int nrows, double *partial, int nb,
                   int rev) {
   switch (j) {
 #define B2_CASE(J) \
   case J:          \
-    k_fb_b2<J><<<nb, ICNT, 0, s>>>(X, st, nrows, partial, rev); \
+    k_fb_b2<J><<<nb, ICNT, 0, s>>>(X, pro, nrows, partial, rev); \
     break;
     FB_CASES(B2_CASE)
 #undef B2_CASE
@@ -1177,12 +1340,12 @@ void launch_fb_b2(hipStream_t s, MvDesc X, int j, const IcgsState *st, int nrows
   }
   LAUNCH_CHECK_();
 }
-void launch_fb_ca(hipStream_t s, MvDesc X, int j, int has_next, const IcgsState *st, int nrows, double *partial,
+void launch_fb_ca(hipStream_t s, MvDesc X, int j, int has_next, const FbPro &pro, int nrows, double *partial,
                   int nb, int rev) {
   switch (j) {
 #define CA_CASE(J) \
   case J:          \
-    k_fb_ca<J><<<nb, ICNT, 0, s>>>(X, has_next, st, nrows, partial, rev); \
+    k_fb_ca<J><<<nb, ICNT, 0, s>>>(X, has_next, pro, nrows, partial, rev); \
     break;
     FB_CASES(CA_CASE)
 #undef CA_CASE
@@ -1191,9 +1354,13 @@ void launch_fb_ca(hipStream_t s, MvDesc X, int j, int has_next, const IcgsState 
   }
   LAUNCH_CHECK_();
 }
-void launch_scale_col(hipStream_t s, MvDesc X, int j, const IcgsState *st, int nrows) {
+void launch_scale_col(hipStream_t s, MvDesc X, int j, const FbPro &pro, int nrows, int nb) {
   if (nrows <= 0) return;
-  k_scale_col<<<cdiv_(nrows, 256), 256, 0, s>>>(X, j, st, nrows);
+  k_scale_col<<<nb, ICNT, 0, s>>>(X, j, pro, nrows);
+  LAUNCH_CHECK_();
+}
+void launch_fb_flush(hipStream_t s, const FbPro &pro) {
+  k_fb_flush<<<1, ICNT, 0, s>>>(pro);
   LAUNCH_CHECK_();
 }
 void launch_reduce_scalar(hipStream_t s, const double *partial, int nblocks, int nv, double *red, IcgsState *st,

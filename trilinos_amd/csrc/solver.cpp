@@ -284,7 +284,16 @@ struct FastIcgs {
   int nblk_tn = 1, nblk_ic = 1;
   double *partial = nullptr, *R1 = nullptr, *R2 = nullptr, *Cout = nullptr, *red = nullptr, *S = nullptr;
   double *sink = nullptr;  // absorbs the padding-lane stores of the fused update kernel
-  IcgsState *st = nullptr;
+  IcgsState *st = nullptr;   // current state (one of stb)
+  IcgsState *stb[2] = {nullptr, nullptr};
+  double *pbuf[2] = {nullptr, nullptr};  // per-workgroup partials, alternating between passes
+  // The reduction + scalar step a pass leaves pending; the next pass takes it in its
+  // prologue (FbPro) -- no separate reduce / scalar launches between the findBasis passes.
+  struct Pending {
+    bool on = false;
+    const double *partial = nullptr;  // nullptr: the all-reduced vector in `red`
+    int nv = 0, s0 = -1, s1 = -1, j = 0, k = 0, complete = 0;
+  } pend;
   double *h = nullptr;  // pinned: state + C
   MvPtr tmpX;
   long long calls = 0, fallbacks = 0;
@@ -296,9 +305,12 @@ struct FastIcgs {
   ~FastIcgs() { release(); }
   void release() {
     if (ctx) hipStreamSynchronize(ctx->stream);
-    for (void *p : {(void *)partial, (void *)R1, (void *)R2, (void *)Cout, (void *)red, (void *)S, (void *)st,
-                    (void *)sink})
+    for (void *p : {(void *)partial, (void *)R1, (void *)R2, (void *)Cout, (void *)red, (void *)S, (void *)stb[0],
+                    (void *)stb[1], (void *)sink, (void *)pbuf[1]})
       if (p) hipFree(p);
+    stb[0] = stb[1] = nullptr;
+    pbuf[0] = pbuf[1] = nullptr;
+    pend = Pending{};
     if (h) hipHostFree(h);
     partial = R1 = R2 = Cout = red = S = sink = nullptr;
     st = nullptr;
@@ -338,7 +350,11 @@ struct FastIcgs {
     const size_t sbytes = sizeof(double) * ((size_t)(nl > 0 ? nl : 1) + 64);
     MIG_HIP(hipMalloc(&S, sbytes));
     MIG_HIP(hipMemset(S, 0, sbytes));  // zero padding row read by the row-pair kernels
-    MIG_HIP(hipMalloc(&st, sizeof(IcgsState)));
+    MIG_HIP(hipMalloc(&stb[0], sizeof(IcgsState)));
+    MIG_HIP(hipMalloc(&stb[1], sizeof(IcgsState)));
+    st = stb[0];
+    pbuf[0] = partial;
+    MIG_HIP(hipMalloc(&pbuf[1], sizeof(double) * (size_t)nblk_ic * 17));
     MIG_HIP(hipHostMalloc(&h, sizeof(IcgsState) + sizeof(double) * (size_t)(lmax + k) * k, hipHostMallocDefault));
     tmpX = MvPtr(mv_create(c, ng, nl, k));
   }
@@ -346,6 +362,56 @@ struct FastIcgs {
   void allreduce(double *d, size_t n) {
     if (ctx->nranks == 1 || n == 0) return;
     ctx->allreduce_async(d, n);
+  }
+
+  // Prologue for the next pass: the pending step (if any), reading the current state and
+  // writing the other buffer, which becomes current.
+  FbPro take_pending() {
+    FbPro p{};
+    p.in = st;
+    p.stage0 = p.stage1 = -1;
+    if (!pend.on) return p;
+    IcgsState *other = st == stb[0] ? stb[1] : stb[0];
+    p.partial = pend.partial;
+    p.red = red;
+    p.nblocks = nblk_ic;
+    p.nv = pend.nv;
+    p.stage0 = pend.s0;
+    p.stage1 = pend.s1;
+    p.j = pend.j;
+    p.k = pend.k;
+    p.complete = pend.complete;
+    p.out = other;
+    st = other;
+    pend.on = false;
+    return p;
+  }
+  // Partials buffer for a pass that may itself read the pending partials in its prologue.
+  double *next_partial() const { return pend.on && pend.partial == pbuf[0] ? pbuf[1] : pbuf[0]; }
+  // After a pass that wrote nv partials per workgroup to `pp`: its reduction and scalar
+  // stage(s) become pending.  On several ranks the partials are reduced and all-reduced now
+  // (the next prologue reads `red`).
+  void set_pending(double *pp, int nv, int s0, int s1, int j, int k, int complete) {
+    pend.on = true;
+    pend.partial = pp;
+    pend.nv = nv;
+    pend.s0 = s0;
+    pend.s1 = s1;
+    pend.j = j;
+    pend.k = k;
+    pend.complete = complete;
+    if (ctx->nranks > 1) {
+      ProfScope ps(ctx, K_REDUCE, 8.0 * nblk_ic * nv);
+      launch_reduce_small(ctx->stream, pp, nblk_ic, nv, red);
+      allreduce(red, (size_t)nv);
+      pend.partial = nullptr;
+    }
+  }
+  // Apply a pending step with no pass after it.
+  void flush_pending() {
+    if (!pend.on) return;
+    const FbPro p = take_pending();
+    launch_fb_flush(ctx->stream, p);
   }
 
   // out (L x kb, leading dim ldo) = A^T B, summed over ranks.
@@ -368,22 +434,6 @@ struct FastIcgs {
     if (ldo == L) allreduce(out, (size_t)L * kb);
   }
 
-  void reduce_small(int nvals) {
-    ProfScope ps(ctx, K_REDUCE, 8.0 * nblk_ic * nvals);
-    launch_reduce_small(ctx->stream, partial, nblk_ic, nvals, red);
-    allreduce(red, (size_t)nvals);
-  }
-  // reduce_small + the scalar step (one launch when there is no all-reduce in between)
-  void reduce_scalar(int nvals, int stage, int j, int k, int complete) {
-    if (ctx->nranks > 1) {
-      reduce_small(nvals);
-      launch_fb_scalar(ctx->stream, st, red, stage, j, k, complete);
-      return;
-    }
-    ProfScope ps(ctx, K_REDUCE, 8.0 * nblk_ic * nvals);
-    launch_reduce_scalar(ctx->stream, partial, nblk_ic, nvals, red, st, stage, j, k, complete);
-  }
-
   // dot: 0 none, 1 column self dots, 3 self dots + <X_0, X_1>
   void nn(const MvDesc &Q, int L, const double *M, int ldm, const MvDesc &X, int k, int dot) {
     if (!dot) {
@@ -391,8 +441,9 @@ struct FastIcgs {
       launch_gemm_nn(ctx->stream, Q, L, M, ldm, X, n_local, -1.0, 1.0);
       return;
     }
+    flush_pending();
     ProfScope ps(ctx, K_GEMM_NN_DOT, 8.0 * n_local * (L + 2.0 * k));
-    launch_gemm_nn_dot(ctx->stream, Q, L, M, ldm, X, n_local, -1.0, 1.0, dot, X, partial, nblk_ic);
+    launch_gemm_nn_dot(ctx->stream, Q, L, M, ldm, X, n_local, -1.0, 1.0, dot, X, pbuf[0], nblk_ic);
   }
 
   // X1 = X - Q C1 (C1 leading dim ldc1) then out = Q^T X1, summed over ranks: one fused pass
@@ -429,45 +480,55 @@ struct FastIcgs {
     return v;
   }
 
-  // head_ready: red already holds [<X_0,X_0>, <X_1,X_1>, ..., <X_0,X_1> at k] from the
-  // closing update of blkOrtho (k_gemm_nn_dot dmode 3), so the a01 pass is skipped.
+  // head_ready: the closing update of blkOrtho (k_gemm_nn_dot dmode 3) left its partials
+  // [<X_0,X_0>, <X_1,X_1>, ..., <X_0,X_1> at k] pending with the dependency test (stage 3);
+  // the first pass applies that and the findBasis head (stage 7) in its prologue, so the
+  // a01 pass is skipped.
   void find_basis(const MvDesc &X, int k, int complete, bool head_ready = false) {
     const double n = (double)n_local;
     if (k == 1) {
       {
         ProfScope ps(ctx, K_FB, 8.0 * n);
-        launch_fb_a(ctx->stream, X, 0, st, n_local, partial, nblk_ic);
+        double *pp = next_partial();
+        const FbPro pro = take_pending();
+        launch_fb_a(ctx->stream, X, 0, pro, n_local, pp, nblk_ic);
+        set_pending(pp, 1, 0, -1, 0, k, complete);
       }
-      reduce_scalar(1, 0, 0, k, complete);
     } else {
       if (head_ready) {
-        launch_fb_scalar(ctx->stream, st, red, 7, 0, k, complete);
+        pend.s1 = 7;  // after stage 3 (set by the closing update)
+        pend.complete = complete;
       } else {
-        {
-          ProfScope ps(ctx, K_FB, 16.0 * n);
-          launch_fb_a01(ctx->stream, X, n_local, partial, nblk_ic);
-        }
-        reduce_scalar(3, 5, 0, k, complete);
+        flush_pending();
+        ProfScope ps(ctx, K_FB, 16.0 * n);
+        launch_fb_a01(ctx->stream, X, n_local, pbuf[0], nblk_ic);
+        set_pending(pbuf[0], 3, 5, -1, 0, k, complete);
       }
       for (int j = 1; j < k; ++j) {
         {
           ProfScope ps(ctx, K_FB, 8.0 * n * (j + 1));
-          launch_fb_b2(ctx->stream, X, j, st, n_local, partial, nblk_ic, fb_rev);
+          double *pp = next_partial();
+          const FbPro pro = take_pending();
+          launch_fb_b2(ctx->stream, X, j, pro, n_local, pp, nblk_ic, fb_rev);
+          set_pending(pp, j + 1, 1, -1, j, k, complete);
         }
-        reduce_scalar(j + 1, 1, j, k, complete);
         const int has_next = j + 1 < k;
         {
           ProfScope ps(ctx, K_FB, 8.0 * n * (j + 3 + has_next));
-          launch_fb_ca(ctx->stream, X, j, has_next, st, n_local, partial, nblk_ic, 0);
+          double *pp = next_partial();
+          const FbPro pro = take_pending();
+          launch_fb_ca(ctx->stream, X, j, has_next, pro, n_local, pp, nblk_ic, 0);
+          set_pending(pp, has_next ? j + 3 : 1, 6, -1, j, k, complete);
         }
-        reduce_scalar(has_next ? j + 3 : 1, 6, j, k, complete);
       }
     }
     ProfScope ps(ctx, K_SCALE, 16.0 * n);
-    launch_scale_col(ctx->stream, X, k - 1, st, n_local);
+    const FbPro pro = take_pending();
+    launch_scale_col(ctx->stream, X, k - 1, pro, n_local, nblk_ic);
   }
 
   void fetch(int L, int k) {
+    flush_pending();
     MIG_HIP(hipMemcpyAsync(h, st, sizeof(IcgsState), hipMemcpyDeviceToHost, ctx->stream));
     if (L > 0)
       MIG_HIP(hipMemcpyAsync(h + sizeof(IcgsState) / sizeof(double), Cout, sizeof(double) * (size_t)L * k,
@@ -497,6 +558,7 @@ struct FastIcgs {
     // DGKS blkOrtho1 decides its second pass on a dot product between the passes: host path
     if (k == 1 && slow->dgks) return slow->project_and_normalize(X, Q, C, ldc, B, ldb);
     ++calls;
+    pend = Pending{};
     launch_state_reset(ctx->stream, st, slow->blk_tol, slow->sing_tol, slow->dgks ? 1 : 0, slow->dep_tol);
     const MvDesc xd = X.desc(), qd = Q.desc();
     if (k == 1) {  // blkOrtho1, then MvDot and MvScale
@@ -504,10 +566,11 @@ struct FastIcgs {
       const bool x1 = nn_then_tn(qd, L, R1, L, xd, 1, R2);
       launch_add_coef(ctx->stream, R1, L, R2, L, Cout, L, L, 1);
       nn(qd, L, x1 ? R2 : Cout, L, xd, 1, 1);
-      reduce_scalar(1, 4, 0, 1, 0);
+      set_pending(pbuf[0], 1, 4, -1, 0, 1, 0);
       {
         ProfScope ps(ctx, K_SCALE, 16.0 * n_local);
-        launch_scale_col(ctx->stream, xd, 0, st, n_local);
+        const FbPro pro = take_pending();
+        launch_scale_col(ctx->stream, xd, 0, pro, n_local, nblk_ic);
       }
       fetch(L, 1);
       for (int i = 0; i < L; ++i) C[i] = hC()[i];
@@ -531,7 +594,7 @@ struct FastIcgs {
     launch_add_coef(ctx->stream, R1, L + k, R2, L, Cout, L, L, k);
     // X2 = X1 - Q C2 (reference order) when X holds X1, else X - Q (C1 + C2)
     nn(qd, L, x1 ? R2 : Cout, L, xd, k, 3);
-    reduce_scalar(k + 1, 3, 0, k, 0);
+    set_pending(pbuf[0], k + 1, 3, -1, 0, k, 0);
     find_basis(xd, k, 0, true);
     fetch(L, k);
     const IcgsState &s = hst();
@@ -557,6 +620,7 @@ struct FastIcgs {
   int normalize(migmres_mv &X, double *B, int ldb) {
     ++calls;
     const int k = X.ncols;
+    pend = Pending{};
     launch_state_reset(ctx->stream, st, slow->blk_tol, slow->sing_tol, slow->dgks ? 1 : 0, slow->dep_tol);
     save_input(X);
     find_basis(X.desc(), k, 1);
