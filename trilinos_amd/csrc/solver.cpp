@@ -295,6 +295,10 @@ struct FastIcgs {
     int nv = 0, s0 = -1, s1 = -1, j = 0, k = 0, complete = 0;
   } pend;
   double *h = nullptr;  // pinned: state + C
+  // Work the caller enqueues behind the state copy before the host waits for it (the next
+  // block's SpMM): the GPU keeps running while the host takes the least-squares update.
+  std::function<void()> before_wait;
+  hipEvent_t ev_fetch = nullptr;
   MvPtr tmpX;
   long long calls = 0, fallbacks = 0;
   bool use_fused = true;  // MIGMRES_NO_FUSED_NN_TN=1 selects the two-kernel form (A/B timing)
@@ -308,6 +312,8 @@ struct FastIcgs {
     for (void *p : {(void *)partial, (void *)R1, (void *)R2, (void *)Cout, (void *)red, (void *)S, (void *)stb[0],
                     (void *)stb[1], (void *)sink, (void *)pbuf[1]})
       if (p) hipFree(p);
+    if (ev_fetch) hipEventDestroy(ev_fetch);
+    ev_fetch = nullptr;
     stb[0] = stb[1] = nullptr;
     pbuf[0] = pbuf[1] = nullptr;
     pend = Pending{};
@@ -350,6 +356,7 @@ struct FastIcgs {
     const size_t sbytes = sizeof(double) * ((size_t)(nl > 0 ? nl : 1) + 64);
     MIG_HIP(hipMalloc(&S, sbytes));
     MIG_HIP(hipMemset(S, 0, sbytes));  // zero padding row read by the row-pair kernels
+    MIG_HIP(hipEventCreateWithFlags(&ev_fetch, hipEventDisableTiming));
     MIG_HIP(hipMalloc(&stb[0], sizeof(IcgsState)));
     MIG_HIP(hipMalloc(&stb[1], sizeof(IcgsState)));
     st = stb[0];
@@ -533,7 +540,13 @@ struct FastIcgs {
     if (L > 0)
       MIG_HIP(hipMemcpyAsync(h + sizeof(IcgsState) / sizeof(double), Cout, sizeof(double) * (size_t)L * k,
                              hipMemcpyDeviceToHost, ctx->stream));
-    MIG_HIP(hipStreamSynchronize(ctx->stream));
+    if (before_wait) {
+      MIG_HIP(hipEventRecord(ev_fetch, ctx->stream));
+      before_wait();
+      MIG_HIP(hipEventSynchronize(ev_fetch));
+    } else {
+      MIG_HIP(hipStreamSynchronize(ctx->stream));
+    }
   }
   const IcgsState &hst() const { return *reinterpret_cast<const IcgsState *>(h); }
   const double *hC() const { return h + sizeof(IcgsState) / sizeof(double); }
@@ -1187,6 +1200,12 @@ struct Engine {
   void iterate(Iter &it) {  // BlockGmresIter::iterate (BelosBlockGmresIter.hpp:659-766)
     const int k = it.k, search = k * it.nb;
     std::vector<double> subH, subH2;
+    // Op V_prev for the next block may already have been computed behind the previous
+    // iteration's state copy (speculatively: unused when the iteration loop ends there or
+    // the orthogonalisation fell back and changed the block; it is counted when used).
+    bool spec_ready = false;
+    const char *se = std::getenv("MIGMRES_SPEC_SPMM");
+    const bool spec_on = !(se && se[0] == '0') && !it.Z.p && !lp.LP && !lp.RP && !(S->p.verbosity & 1);
     while (!check(it) && it.cur_dim + k <= search) {
       ++it.num_iters;
       ++S->n_block_iters;
@@ -1198,9 +1217,27 @@ struct Engine {
         Znext = view(*it.Z, c, k);
         lp.apply_right_prec(*Vprev, *Znext);
         lp.op(*Znext, *Vnext);
+      } else if (spec_ready) {
+        ++S->n_apply;  // OPT::Apply(A) done ahead
       } else {
         lp.apply(*Vprev, *Vnext);
       }
+      spec_ready = false;
+      MvPtr Vnn;
+      bool spec_issued = false;
+      const bool spec = spec_on && S->use_fast && S->fast.supports(k) && lcl + k <= search;
+      if (spec) {
+        Vnn = view(*it.V, lcl + k, k);
+        S->fast.before_wait = [&] {
+          crs_apply(*lp.A, *Vnext, *Vnn, 1.0, 0.0);
+          spec_issued = true;
+        };
+      }
+      struct HookReset {
+        std::function<void()> &f;
+        ~HookReset() { f = nullptr; }
+      } hook_reset{S->fast.before_wait};
+      const long long fb0 = S->fast.fallbacks;
       MvPtr Q = view(*it.V, 0, lcl);
       subH.assign((size_t)lcl * k, 0.0);
       subH2.assign((size_t)k * k, 0.0);
@@ -1222,6 +1259,8 @@ struct Engine {
                            ? S->fast.project_and_normalize(*Vnext, *Q, subH.data(), lcl, subH2.data(), k, &regen)
                            : S->ortho.project_and_normalize(*Vnext, *Q, subH.data(), lcl, subH2.data(), k);
       S->t_ortho += since(t0);
+      S->fast.before_wait = nullptr;
+      spec_ready = spec_issued && S->fast.fallbacks == fb0 && rank == k;
       for (int j = 0; j < k; ++j) {
         for (int i = 0; i < lcl; ++i) it.Rat(i, c + j) = subH[(size_t)i + (size_t)j * lcl];
         for (int i = 0; i < k; ++i) it.Rat(lcl + i, c + j) = subH2[(size_t)i + (size_t)j * k];
