@@ -1,6 +1,6 @@
 source ./tools_gpu_check.sh
 export TMPDIR=/tmp
-P=${PROF:-r1d}
+P=${PROF:-r1e}
 step 600 bench_$P.log python bench.py
 step 900 rocprof_stats_$P.log rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof_$P -o run -- python3 bench.py --no-cpu-baseline
 step 900 rocprof_fetch_$P.log rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d gpurun_out/prof_${P}_fetch -o run --kernel-include-regex "gemm_tn|nn_tn|gemm_nn|spmm|k_fb" -- python3 bench.py --no-cpu-baseline --no-profile
