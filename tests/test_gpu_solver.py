@@ -266,3 +266,24 @@ def test_dgks_orsirr1_reference_run(comm):
     assert f"{rel:.5e}" == "9.94786e-06"
     ref = ob.solve(Aor.apply, b[:, None], dict(params, Orthogonalization="DGKS"))
     _hist_close(sm.residualHistory(), ref["history"], ref["restarts"])
+
+
+@pytest.mark.parametrize("env", [{"MIGMRES_FB_GRAM": "0"}, {"MIGMRES_FB_GRAM_GATE": "2"},
+                                 {"MIGMRES_FB_GRAM_FUSE": "0"}])
+def test_gram_findbasis_against_column_passes(comm, monkeypatch, env):
+    """findBasis in Gram form (CholQR2 of the block with the reference's dependency tests on
+    its pivots; the default for ICGS with 2 <= k <= 8) against the column-by-column passes
+    (MIGMRES_FB_GRAM=0), against its own gate hand-back (gate 2: every block goes to the
+    column passes, after the speculative SpMM has read it) and against its unfused form: the
+    same solver decisions and iteration counts, histories within 1e-12 of ||r0|| per cycle."""
+    params = {"Block Size": 4, "Num Blocks": 10, "Maximum Iterations": 400, "Maximum Restarts": 40,
+              "Convergence Tolerance": 1e-9, "Orthogonalization": "ICGS"}
+    sm, ret, X, _, _ = _device_solve(comm, "Laplace3D", (14, 13, 12), 4, 7, params)
+    for key, v in env.items():
+        monkeypatch.setenv(key, v)
+    sm2, ret2, X2, _, _ = _device_solve(comm, "Laplace3D", (14, 13, 12), 4, 7, params)
+    c = sm.counters()
+    assert ret2 == ret and sm2.getNumIters() == sm.getNumIters()
+    assert sm2.counters() == c
+    _hist_close(sm2.residualHistory(), sm.residualHistory(), c["restarts"])
+    np.testing.assert_allclose(X2, X, rtol=0, atol=1e-8 * np.abs(X).max())

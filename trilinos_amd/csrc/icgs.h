@@ -15,7 +15,23 @@ struct IcgsState {
   int failed;  // first findBasis column found dependent, -1 if none
   int dgks;    // 1: DGKSOrthoManager findBasis (second projection only under dep_tol)
   double dep_tol;
+  int gram_skip;  // findBasis in Gram form handed the block back to the column passes
+  int gram_pad_;
 };
+
+// findBasis in Gram form (icgs.hip; ICGS with two passes, 2 <= k <= 8).  The partial-writing
+// launchers return their number of workgroups (rows of partials, at most 1024), stored
+// value-major (partial[i * nb + b]): the packed upper triangle of the k x k Gram matrix.
+// w: 768 doubles of device scratch (T1, T2, R1).
+int launch_gemm_nn_gram(hipStream_t s, MvDesc A, int L, const double *M, int ldm, MvDesc X, int nrows,
+                        double *partial);
+int launch_fbg_gram(hipStream_t s, MvDesc X, int k, int nrows, double *partial, int rev);
+int launch_fbg_a(hipStream_t s, MvDesc X, int k, int nrows, const IcgsState *st, const double *w, double *partial,
+                 int rev);
+void launch_fbg_b(hipStream_t s, MvDesc X, int k, int nrows, const IcgsState *st, const double *w, int rev);
+// stage 0: sums of the partials only (-> sums); 1: dependency test, R1, gate, T1; 2: R2, T2, B
+void launch_fbg_chol(hipStream_t s, const double *partial, int nblocks, int k, int stage, IcgsState *st, double *w,
+                     double gate, double *sums);
 
 // Pass prologue: the reduction + scalar step still pending from the previous pass, taken by
 // every workgroup of the next pass from the previous pass's per-workgroup partials (one

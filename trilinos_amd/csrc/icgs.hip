@@ -1387,4 +1387,367 @@ void launch_add_coef(hipStream_t s, const double *C1, int ld1, const double *C2,
   LAUNCH_CHECK_();
 }
 
+// -------------------------------------------------------------------------------------
+// findBasis in Gram form: ICGS with two passes, completeBasis = false, 2 <= k <= 8 -- the
+// blkOrtho -> findBasis step of every block iteration (FastIcgs::find_basis_gram).
+//
+// Column-by-column CGS2 over the block (BelosICGSOrthoManager.hpp:1002-1222) computes, in
+// exact arithmetic, B = R with R^T R = X^T X (the Cholesky factor of the block's Gram
+// matrix, positive diagonal) and X <- X R^{-1}; its dependency ratio newDot_j / oldDot_j
+// (:1190) is R_jj^2 / (X^T X)_jj.  Here the block is streamed twice after the closing
+// update instead of in 2k - 1 passes over 2 .. k + 2 columns (24Nk bytes against about 8N x
+// 92 at k = 8):
+//   k_gemm_nn_gram  blkOrtho's closing update X <- X - Q M with the partials of G1 = X^T X
+//                   (k_fbg_gram: G1 in a read pass of its own, for the unfused A/B form)
+//   k_fbg_chol 1    blkOrtho's dependency test on diag(G1) (:1433-1442), R1 = chol(G1),
+//                   the gate, T1 = R1^{-1}
+//   k_fbg_a         partials of G2 = Y^T Y, Y = X T1 formed in registers    (read k columns)
+//   k_fbg_chol 2    R2 = chol(G2), T2 = R2^{-1}, B = R2 R1
+//   k_fbg_b         X <- (X T1) T2, Y re-formed bit for bit          (read + write k columns)
+// -- CholQR2 (the reference's s-step GMRES normalises with CholQR too:
+// Belos_Tpetra_GmresSstep.hpp:16, 162-168), as accurate as CGS2 on a well-conditioned block.
+// The gate keeps it to such blocks: a pivot ratio R1_jj^2 / G1_jj below `gate` (100 blk_tol
+// by default, far above the reference's own threshold) sets gram_skip, k_fbg_a / k_fbg_b
+// return at once, and the host runs the column passes on the block, which still holds X - Q M.
+// Packed upper triangle: entry (i, j), i <= j, at j (j + 1) / 2 + i.  Partials are stored
+// value-major (partial[i * gridDim.x + b]) so that k_fbg_chol reads them coalesced.
+// -------------------------------------------------------------------------------------
+constexpr int FBG_NT = 256;
+
+template <int NV>
+__device__ __forceinline__ void fbg_reduce_store(double (&v)[NV], double *partial) {
+  __shared__ double red[FBG_NT / 64][NV];
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    double x = v[i];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off, 64);
+    if (l == 0) red[w][i] = x;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < NV; i += FBG_NT)
+    partial[(long long)i * gridDim.x + blockIdx.x] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
+}
+
+__device__ __forceinline__ long long fbg_row(long long p, long long np, int rev) {
+  return 2 * (rev ? np - 1 - p : p);
+}
+
+template <int K>
+__device__ __forceinline__ void fbg_gram_acc(const d2 (&x)[K], double (&g)[K * (K + 1) / 2]) {
+#pragma unroll
+  for (int j = 0; j < K; ++j)
+#pragma unroll
+    for (int i = 0; i <= j; ++i) g[j * (j + 1) / 2 + i] += x[i].x * x[j].x + x[i].y * x[j].y;
+}
+
+// x <- x T, T upper triangular (T[i + 16 c]); in place from the last column down (column c
+// of the product reads x_0 .. x_c only).
+template <int K>
+__device__ __forceinline__ void fbg_apply(d2 (&x)[K], const double (&T)[16 * K]) {
+#pragma unroll
+  for (int c = K - 1; c >= 0; --c) {
+    d2 a = x[0] * T[16 * c];
+#pragma unroll
+    for (int i = 1; i <= c; ++i) a += x[i] * T[i + 16 * c];
+    x[c] = a;
+  }
+}
+
+// Rows past nrows are the zero padding of the multivectors (ld > nrows): an odd tail's second
+// row reads as zero, adds nothing to a Gram matrix and is not stored.
+template <int K>
+__global__ __launch_bounds__(FBG_NT) void k_gemm_nn_gram(MvDesc A, int L, const double *__restrict__ M, int ldm,
+                                                        MvDesc X, int nrows, double *__restrict__ partial) {
+  extern __shared__ __attribute__((aligned(16))) double Mg[];  // L x K
+  for (int e = threadIdx.x; e < L * K; e += FBG_NT) {
+    const int j = e / K, c = e % K;
+    Mg[e] = M[j + (long long)c * ldm];
+  }
+  __syncthreads();
+  constexpr int NV = K * (K + 1) / 2, NB = 8;
+  double g[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) g[i] = 0.0;
+  for (long long r = 2LL * ((long long)blockIdx.x * FBG_NT + threadIdx.x); r < nrows;
+       r += 2LL * gridDim.x * FBG_NT) {
+    d2 acc[K];
+#pragma unroll
+    for (int c = 0; c < K; ++c) acc[c] = d2{0.0, 0.0};
+    int j = 0;
+    for (; j + NB <= L; j += NB) {
+      d2 v[NB];
+#pragma unroll
+      for (int u = 0; u < NB; ++u) v[u] = *(const d2 *)(colp_(A, j + u) + r);
+#pragma unroll
+      for (int u = 0; u < NB; ++u)
+#pragma unroll
+        for (int c = 0; c < K; ++c) acc[c] += v[u] * Mg[(j + u) * K + c];
+    }
+    for (; j < L; ++j) {
+      const d2 v = *(const d2 *)(colp_(A, j) + r);
+#pragma unroll
+      for (int c = 0; c < K; ++c) acc[c] += v * Mg[j * K + c];
+    }
+    const bool two = r + 1 < nrows;
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+      double *xp = colp_(X, c) + r;
+      acc[c] = *(const d2 *)xp - acc[c];
+      st_pair(xp, acc[c].x, acc[c].y, two);
+    }
+    fbg_gram_acc<K>(acc, g);
+  }
+  fbg_reduce_store<NV>(g, partial);
+}
+
+template <int K>
+__global__ __launch_bounds__(FBG_NT) void k_fbg_gram(MvDesc X, int nrows, double *__restrict__ partial, int rev) {
+  constexpr int NV = K * (K + 1) / 2;
+  double g[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) g[i] = 0.0;
+  const long long np = ((long long)nrows + 1) / 2, stride = (long long)gridDim.x * FBG_NT;
+  for (long long p = (long long)blockIdx.x * FBG_NT + threadIdx.x; p < np; p += stride) {
+    const long long r = fbg_row(p, np, rev);
+    d2 x[K];
+#pragma unroll
+    for (int c = 0; c < K; ++c) x[c] = *(const d2 *)(colp_(X, c) + r);
+    fbg_gram_acc<K>(x, g);
+  }
+  fbg_reduce_store<NV>(g, partial);
+}
+
+template <int K>
+__global__ __launch_bounds__(FBG_NT) void k_fbg_a(MvDesc X, int nrows, const IcgsState *__restrict__ st,
+                                                 const double *__restrict__ w, double *__restrict__ partial, int rev) {
+  if (st->gram_skip) return;
+  __shared__ double T1[16 * K];
+  for (int e = threadIdx.x; e < 16 * K; e += FBG_NT) T1[e] = w[e];
+  __syncthreads();
+  constexpr int NV = K * (K + 1) / 2;
+  double g[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) g[i] = 0.0;
+  const long long np = ((long long)nrows + 1) / 2, stride = (long long)gridDim.x * FBG_NT;
+  for (long long p = (long long)blockIdx.x * FBG_NT + threadIdx.x; p < np; p += stride) {
+    const long long r = fbg_row(p, np, rev);
+    d2 x[K];
+#pragma unroll
+    for (int c = 0; c < K; ++c) x[c] = *(const d2 *)(colp_(X, c) + r);
+    fbg_apply<K>(x, T1);
+    fbg_gram_acc<K>(x, g);
+  }
+  fbg_reduce_store<NV>(g, partial);
+}
+
+template <int K>
+__global__ __launch_bounds__(FBG_NT) void k_fbg_b(MvDesc X, int nrows, const IcgsState *__restrict__ st,
+                                                 const double *__restrict__ w, int rev) {
+  if (st->gram_skip) return;
+  __shared__ double T1[16 * K], T2[16 * K];
+  for (int e = threadIdx.x; e < 16 * K; e += FBG_NT) {
+    T1[e] = w[e];
+    T2[e] = w[256 + e];
+  }
+  __syncthreads();
+  const long long np = ((long long)nrows + 1) / 2, stride = (long long)gridDim.x * FBG_NT;
+  for (long long p = (long long)blockIdx.x * FBG_NT + threadIdx.x; p < np; p += stride) {
+    const long long r = fbg_row(p, np, rev);
+    d2 x[K];
+#pragma unroll
+    for (int c = 0; c < K; ++c) x[c] = *(const d2 *)(colp_(X, c) + r);
+    fbg_apply<K>(x, T1);
+    fbg_apply<K>(x, T2);
+    const bool two = r + 1 < nrows;
+#pragma unroll
+    for (int c = 0; c < K; ++c) st_pair(colp_(X, c) + r, x[c].x, x[c].y, two);
+  }
+}
+
+// One workgroup: the fixed-order sum of the partial rows, then thread 0 takes the step
+// (the k x k factorisations; R, T in LDS).
+__global__ __launch_bounds__(256) void k_fbg_chol(const double *__restrict__ partial, int nblocks, int k, int stage,
+                                                  IcgsState *st, double *__restrict__ w, double gate,
+                                                  double *__restrict__ sums) {
+  const int nv = k * (k + 1) / 2;
+  double v[36];
+#pragma unroll
+  for (int i = 0; i < 36; ++i) v[i] = 0.0;
+  for (int b = threadIdx.x; b < nblocks; b += 256) {
+    double x[36];
+#pragma unroll
+    for (int i = 0; i < 36; ++i) x[i] = partial[(long long)(i < nv ? i : nv - 1) * nblocks + b];
+#pragma unroll
+    for (int i = 0; i < 36; ++i) v[i] += i < nv ? x[i] : 0.0;
+  }
+  __shared__ double red[4][36];
+  __shared__ double G[36], R[64], T[64];
+  const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < 36; ++i) {
+    double x = v[i];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off, 64);
+    if (l == 0) red[wv][i] = x;
+  }
+  __syncthreads();
+  if (threadIdx.x < nv) {
+    const int i = threadIdx.x;
+    G[i] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
+    if (sums) sums[i] = G[i];
+  }
+  __syncthreads();
+  if (stage == 0 || threadIdx.x != 0) return;
+  if (stage == 2 && st->gram_skip) return;
+  if (stage == 1) {
+    st->gram_skip = 0;
+    for (int c = 0; c < k; ++c)
+      if (fabs(G[c * (c + 1) / 2 + c]) < fabs(st->blk_old[c] * st->blk_tol)) st->dep = 1.0;
+  }
+  // G = R^T R, R upper triangular with a positive diagonal; pivot ratios against the gate
+  for (int j = 0; j < k; ++j) {
+    const double gjj = G[j * (j + 1) / 2 + j];
+    double s = gjj;
+    for (int i = 0; i < j; ++i) s -= R[i + 8 * j] * R[i + 8 * j];
+    if (!(gjj > 0.0) || !(s >= gate * gjj)) {
+      st->gram_skip = 1;
+      return;
+    }
+    const double d = sqrt(s);
+    R[j + 8 * j] = d;
+    for (int c = j + 1; c < k; ++c) {
+      double t = G[c * (c + 1) / 2 + j];
+      for (int i = 0; i < j; ++i) t -= R[i + 8 * j] * R[i + 8 * c];
+      R[j + 8 * c] = t / d;
+    }
+  }
+  // T = R^{-1}
+  for (int c = 0; c < k; ++c) {
+    T[c + 8 * c] = 1.0 / R[c + 8 * c];
+    for (int i = c - 1; i >= 0; --i) {
+      double t = 0.0;
+      for (int m = i + 1; m <= c; ++m) t += R[i + 8 * m] * T[m + 8 * c];
+      T[i + 8 * c] = -t / R[i + 8 * i];
+    }
+  }
+  double *Tout = w + (stage == 1 ? 0 : 256);
+  for (int c = 0; c < k; ++c)
+    for (int i = 0; i <= c; ++i) Tout[i + 16 * c] = T[i + 8 * c];
+  if (stage == 1) {
+    for (int c = 0; c < k; ++c)
+      for (int i = 0; i <= c; ++i) w[512 + i + 16 * c] = R[i + 8 * c];
+  } else {
+    // B = R2 R1: the reference's B (projection coefficients above the diagonal, the norms on it)
+    for (int c = 0; c < k; ++c)
+      for (int i = 0; i <= c; ++i) {
+        double t = 0.0;
+        for (int m = i; m <= c; ++m) t += R[i + 8 * m] * w[512 + m + 16 * c];
+        st->B[i + 16 * c] = t;
+      }
+  }
+}
+
+// Workgroups of a Gram-form pass: as many as are resident at once (one round, so the
+// grid-stride sweeps end together), at most 1024 partial rows, at least 512 row pairs each.
+template <class F>
+static int fbg_resident(F kern, size_t lds) {
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, FBG_NT, lds) != hipSuccess || per_cu < 1)
+    per_cu = 2;
+  const long long b = (long long)per_cu * cu_count();
+  return b > 1024 ? 1024 : (int)b;
+}
+static int fbg_nb(int resident, int nrows) {
+  const long long cap = (((long long)nrows + 1) / 2 + 511) / 512;
+  const long long b = resident < cap ? resident : cap;
+  return b < 1 ? 1 : (int)b;
+}
+
+#define FBG_CASES(M) M(2) M(3) M(4) M(5) M(6) M(7) M(8)
+
+int launch_gemm_nn_gram(hipStream_t s, MvDesc A, int L, const double *M, int ldm, MvDesc X, int nrows,
+                        double *partial) {
+  const int k = X.ncols;
+  if (k < 2 || k > 8 || L < 0 || L > 1024) throw Error(MIGMRES_EINVAL, "gemm_nn_gram: 2 <= k <= 8 and L <= 1024");
+  const size_t lds = sizeof(double) * (size_t)(L > 0 ? L : 1) * k;
+  static int occ[9][1025];
+  int nb = 1;
+  switch (k) {
+#define NNG_CASE(K)                                                              \
+  case K:                                                                        \
+    if (!occ[K][L]) occ[K][L] = fbg_resident(k_gemm_nn_gram<K>, lds);           \
+    nb = fbg_nb(occ[K][L], nrows);                                               \
+    k_gemm_nn_gram<K><<<nb, FBG_NT, lds, s>>>(A, L, M, ldm, X, nrows, partial); \
+    break;
+    FBG_CASES(NNG_CASE)
+#undef NNG_CASE
+  }
+  LAUNCH_CHECK_();
+  return nb;
+}
+
+int launch_fbg_gram(hipStream_t s, MvDesc X, int k, int nrows, double *partial, int rev) {
+  static int occ[9];
+  int nb = 1;
+  switch (k) {
+#define FG_CASE(K)                                                 \
+  case K:                                                          \
+    if (!occ[K]) occ[K] = fbg_resident(k_fbg_gram<K>, 0);          \
+    nb = fbg_nb(occ[K], nrows);                                    \
+    k_fbg_gram<K><<<nb, FBG_NT, 0, s>>>(X, nrows, partial, rev);   \
+    break;
+    FBG_CASES(FG_CASE)
+#undef FG_CASE
+    default:
+      throw Error(MIGMRES_EINVAL, "fbg_gram: 2 <= k <= 8");
+  }
+  LAUNCH_CHECK_();
+  return nb;
+}
+
+int launch_fbg_a(hipStream_t s, MvDesc X, int k, int nrows, const IcgsState *st, const double *w, double *partial,
+                 int rev) {
+  static int occ[9];
+  int nb = 1;
+  switch (k) {
+#define FA_CASE(K)                                                       \
+  case K:                                                                \
+    if (!occ[K]) occ[K] = fbg_resident(k_fbg_a<K>, 0);                   \
+    nb = fbg_nb(occ[K], nrows);                                          \
+    k_fbg_a<K><<<nb, FBG_NT, 0, s>>>(X, nrows, st, w, partial, rev);     \
+    break;
+    FBG_CASES(FA_CASE)
+#undef FA_CASE
+    default:
+      throw Error(MIGMRES_EINVAL, "fbg_a: 2 <= k <= 8");
+  }
+  LAUNCH_CHECK_();
+  return nb;
+}
+
+void launch_fbg_b(hipStream_t s, MvDesc X, int k, int nrows, const IcgsState *st, const double *w, int rev) {
+  static int occ[9];
+  switch (k) {
+#define FB2_CASE(K)                                                               \
+  case K:                                                                         \
+    if (!occ[K]) occ[K] = fbg_resident(k_fbg_b<K>, 0);                            \
+    k_fbg_b<K><<<fbg_nb(occ[K], nrows), FBG_NT, 0, s>>>(X, nrows, st, w, rev);    \
+    break;
+    FBG_CASES(FB2_CASE)
+#undef FB2_CASE
+    default:
+      throw Error(MIGMRES_EINVAL, "fbg_b: 2 <= k <= 8");
+  }
+  LAUNCH_CHECK_();
+}
+
+void launch_fbg_chol(hipStream_t s, const double *partial, int nblocks, int k, int stage, IcgsState *st, double *w,
+                     double gate, double *sums) {
+  if (k < 2 || k > 8) throw Error(MIGMRES_EINVAL, "fbg_chol: 2 <= k <= 8");
+  k_fbg_chol<<<1, 256, 0, s>>>(partial, nblocks, k, stage, st, w, gate, sums);
+  LAUNCH_CHECK_();
+}
+
 }  // namespace migmres

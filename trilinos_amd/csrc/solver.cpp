@@ -109,15 +109,16 @@ struct Icgs {
 
   int normalize(migmres_mv &X, double *B, int ldb) { return find_basis(X, B, ldb, true); }
 
-  // blkOrtho1 (BelosICGSOrthoManager.hpp:1231-1322; DGKS: BelosDGKSOrthoManager.hpp:1245-1321)
+  // blkOrtho1 (BelosICGSOrthoManager.hpp:1231-1322; DGKS: BelosDGKSOrthoManager.hpp:1245-1321), and
+  // the projection passes of blkOrtho (ICGS :1328-1445, DGKS :1373-1490, the same for both)
   void blk_ortho1(migmres_mv &X, migmres_mv &Q, double *C, int ldc) {
     const int L = Q.ncols, k = X.ncols;
     double old_dot = 0.0;
-    if (dgks) old_dot = dot1(X, X);
+    if (dgks && k == 1) old_dot = dot1(X, X);
     mv_trans_mv(1.0, Q, X, C, ldc);
     mv_times_mat_add_mv(-1.0, Q, C, ldc, 1.0, X);
     std::vector<double> C2((size_t)L * k);
-    if (dgks) {
+    if (dgks && k == 1) {  // DGKS blkOrtho on k > 1 columns: the passes below
       const double new_dot = dot1(X, X);
       if (std::sqrt(std::fabs(new_dot)) < dep_tol * std::sqrt(std::fabs(old_dot))) {
         mv_trans_mv(1.0, Q, X, C2.data(), L);
@@ -305,6 +306,30 @@ struct FastIcgs {
   int fb_rev = 1;         // findBasis b2 passes sweep rows top-down (MIGMRES_FB_REV=0: all bottom-up)
   bool x1_store = false;  // fused pass writes X1 back (MIGMRES_NN_TN_STORE=1, A/B timing)
   int nt_cache[257][4] = {};
+  // findBasis in Gram form (icgs.hip k_fbg_*; ICGS with two passes, 2 <= k <= 8).
+  // MIGMRES_FB_GRAM=0 keeps the column passes; MIGMRES_FB_GRAM_FUSE=0 takes G1 in a pass of
+  // its own instead of in the closing update; MIGMRES_FB_GRAM_GATE overrides the pivot-ratio
+  // gate (default 100 blk_tol; a value above 1 hands every block to the column passes).
+  struct GramBufs {
+    double *part = nullptr, *sum = nullptr, *w = nullptr;
+    ~GramBufs() {
+      for (double *p : {part, sum, w})
+        if (p) hipFree(p);
+    }
+  } gb;
+  bool gram_on = [] {
+    const char *e = std::getenv("MIGMRES_FB_GRAM");
+    return !(e && e[0] == '0');
+  }();
+  bool gram_fuse = [] {
+    const char *e = std::getenv("MIGMRES_FB_GRAM_FUSE");
+    return !(e && e[0] == '0');
+  }();
+  double gram_gate = [] {
+    const char *e = std::getenv("MIGMRES_FB_GRAM_GATE");
+    return e ? std::atof(e) : 0.0;
+  }();
+  long long gram_calls = 0, gram_skips = 0;
 
   ~FastIcgs() { release(); }
   void release() {
@@ -534,6 +559,49 @@ struct FastIcgs {
     launch_scale_col(ctx->stream, X, k - 1, pro, n_local, nblk_ic);
   }
 
+  bool gram_ok(int L, int k) const {
+    return gram_on && !slow->dgks && slow->steps == 2 && k >= 2 && k <= 8 && L >= 1 && L <= 1024 && L * k <= 7680;
+  }
+  void gram_alloc() {
+    if (gb.part) return;
+    MIG_HIP(hipMalloc(&gb.part, sizeof(double) * 1024 * 36));
+    MIG_HIP(hipMalloc(&gb.sum, sizeof(double) * 64));
+    MIG_HIP(hipMalloc(&gb.w, sizeof(double) * 768));
+  }
+  // findBasis in Gram form (icgs.hip): CholQR2 of the block with the reference's dependency
+  // tests on its pivots.  nb1: rows of G1 partials the closing update (k_gemm_nn_gram) left
+  // in gb.part, 0 to take G1 in a pass of its own.
+  void find_basis_gram(const MvDesc &X, int k, int nb1) {
+    ++gram_calls;
+    const int nv = k * (k + 1) / 2;
+    const double n = (double)n_local;
+    const double gate = gram_gate > 0.0 ? gram_gate : 100.0 * slow->blk_tol;
+    auto chol = [&](int stage, int nb) {
+      ProfScope ps(ctx, K_REDUCE, 8.0 * nb * nv);
+      if (ctx->nranks > 1) {
+        launch_fbg_chol(ctx->stream, gb.part, nb, k, 0, st, gb.w, gate, gb.sum);
+        allreduce(gb.sum, (size_t)nv);
+        launch_fbg_chol(ctx->stream, gb.sum, 1, k, stage, st, gb.w, gate, nullptr);
+      } else {
+        launch_fbg_chol(ctx->stream, gb.part, nb, k, stage, st, gb.w, gate, nullptr);
+      }
+    };
+    const int rev = nb1 ? 1 : 0;  // sweep directions alternate from pass to pass
+    if (!nb1) {
+      ProfScope ps(ctx, K_FB, 8.0 * n * k);
+      nb1 = launch_fbg_gram(ctx->stream, X, k, n_local, gb.part, 1);
+    }
+    chol(1, nb1);
+    int nb2;
+    {
+      ProfScope ps(ctx, K_FB, 8.0 * n * k);
+      nb2 = launch_fbg_a(ctx->stream, X, k, n_local, st, gb.w, gb.part, rev);
+    }
+    chol(2, nb2);
+    ProfScope ps(ctx, K_FB, 16.0 * n * k);
+    launch_fbg_b(ctx->stream, X, k, n_local, st, gb.w, 1 - rev);
+  }
+
   void fetch(int L, int k) {
     flush_pending();
     MIG_HIP(hipMemcpyAsync(h, st, sizeof(IcgsState), hipMemcpyDeviceToHost, ctx->stream));
@@ -606,12 +674,38 @@ struct FastIcgs {
     const bool x1 = nn_then_tn(qd, L, R1, L + k, xd, k, R2);
     launch_add_coef(ctx->stream, R1, L + k, R2, L, Cout, L, L, k);
     // X2 = X1 - Q C2 (reference order) when X holds X1, else X - Q (C1 + C2)
-    nn(qd, L, x1 ? R2 : Cout, L, xd, k, 3);
-    set_pending(pbuf[0], k + 1, 3, -1, 0, k, 0);
-    find_basis(xd, k, 0, true);
+    const double *M2 = x1 ? R2 : Cout;
+    const bool gram = gram_ok(L, k);
+    if (gram) {
+      gram_alloc();
+      flush_pending();
+      int nb1 = 0;
+      {
+        ProfScope ps(ctx, K_GEMM_NN_DOT, 8.0 * n_local * (L + 2.0 * k));
+        if (gram_fuse)
+          nb1 = launch_gemm_nn_gram(ctx->stream, qd, L, M2, L, xd, n_local, gb.part);
+        else
+          launch_gemm_nn(ctx->stream, qd, L, M2, L, xd, n_local, -1.0, 1.0);
+      }
+      find_basis_gram(xd, k, nb1);
+    } else {
+      nn(qd, L, M2, L, xd, k, 3);
+      set_pending(pbuf[0], k + 1, 3, -1, 0, k, 0);
+      find_basis(xd, k, 0, true);
+    }
     fetch(L, k);
+    if (hst().neg != 0.0) throw Error(MIGMRES_ESTATE, "ICGS: negative definiteness in inner product");
+    if (gram && hst().dep == 0.0 && hst().gram_skip) {
+      // a column too close to the span of the others for the Gram form: the column passes on
+      // the block, which the skipped passes left holding X2
+      ++gram_skips;
+      ++fallbacks;  // not the final block when the speculative SpMM (if any) read it
+      before_wait = nullptr;
+      find_basis(xd, k, 0, false);
+      fetch(L, k);
+      if (hst().neg != 0.0) throw Error(MIGMRES_ESTATE, "ICGS: negative definiteness in inner product");
+    }
     const IcgsState &s = hst();
-    if (s.neg != 0.0) throw Error(MIGMRES_ESTATE, "ICGS: negative definiteness in inner product");
     if (s.dep != 0.0 || s.failed >= 0) {
       ++fallbacks;
       if (regen)
