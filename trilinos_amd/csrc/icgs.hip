@@ -1566,34 +1566,33 @@ __global__ __launch_bounds__(FBG_NT) void k_fbg_b(MvDesc X, int nrows, const Icg
   }
 }
 
-// One workgroup: the fixed-order sum of the partial rows, then thread 0 takes the step
-// (the k x k factorisations; R, T in LDS).
-__global__ __launch_bounds__(256) void k_fbg_chol(const double *__restrict__ partial, int nblocks, int k, int stage,
+// One workgroup: the fixed-order sum of the partial rows, then thread 0 takes the step.
+// Templated on k so that G, R and T are register arrays (fully unrolled): the k x k
+// factorisations are a chain of dependent operations, which through LDS cost tens of us.
+template <int K>
+__global__ __launch_bounds__(256) void k_fbg_chol(const double *__restrict__ partial, int nblocks, int stage,
                                                   IcgsState *st, double *__restrict__ w, double gate,
                                                   double *__restrict__ sums) {
-  const int nv = k * (k + 1) / 2;
-  double v[36];
+  constexpr int NV = K * (K + 1) / 2;
+  double v[NV];
 #pragma unroll
-  for (int i = 0; i < 36; ++i) v[i] = 0.0;
+  for (int i = 0; i < NV; ++i) v[i] = 0.0;
   for (int b = threadIdx.x; b < nblocks; b += 256) {
-    double x[36];
 #pragma unroll
-    for (int i = 0; i < 36; ++i) x[i] = partial[(long long)(i < nv ? i : nv - 1) * nblocks + b];
-#pragma unroll
-    for (int i = 0; i < 36; ++i) v[i] += i < nv ? x[i] : 0.0;
+    for (int i = 0; i < NV; ++i) v[i] += partial[(long long)i * nblocks + b];
   }
-  __shared__ double red[4][36];
-  __shared__ double G[36], R[64], T[64];
+  __shared__ double red[4][NV];
+  __shared__ double G[NV];
   const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
-  for (int i = 0; i < 36; ++i) {
+  for (int i = 0; i < NV; ++i) {
     double x = v[i];
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off, 64);
     if (l == 0) red[wv][i] = x;
   }
   __syncthreads();
-  if (threadIdx.x < nv) {
+  if (threadIdx.x < NV) {
     const int i = threadIdx.x;
     G[i] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
     if (sums) sums[i] = G[i];
@@ -1601,49 +1600,76 @@ __global__ __launch_bounds__(256) void k_fbg_chol(const double *__restrict__ par
   __syncthreads();
   if (stage == 0 || threadIdx.x != 0) return;
   if (stage == 2 && st->gram_skip) return;
+  double g[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) g[i] = G[i];
   if (stage == 1) {
     st->gram_skip = 0;
-    for (int c = 0; c < k; ++c)
-      if (fabs(G[c * (c + 1) / 2 + c]) < fabs(st->blk_old[c] * st->blk_tol)) st->dep = 1.0;
+    bool dep = false;
+#pragma unroll
+    for (int c = 0; c < K; ++c) dep = dep || fabs(g[c * (c + 1) / 2 + c]) < fabs(st->blk_old[c] * st->blk_tol);
+    if (dep) st->dep = 1.0;
   }
   // G = R^T R, R upper triangular with a positive diagonal; pivot ratios against the gate
-  for (int j = 0; j < k; ++j) {
-    const double gjj = G[j * (j + 1) / 2 + j];
+  double R[K][K], T[K][K];
+  bool ok = true;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const double gjj = g[j * (j + 1) / 2 + j];
     double s = gjj;
-    for (int i = 0; i < j; ++i) s -= R[i + 8 * j] * R[i + 8 * j];
-    if (!(gjj > 0.0) || !(s >= gate * gjj)) {
-      st->gram_skip = 1;
-      return;
-    }
-    const double d = sqrt(s);
-    R[j + 8 * j] = d;
-    for (int c = j + 1; c < k; ++c) {
-      double t = G[c * (c + 1) / 2 + j];
-      for (int i = 0; i < j; ++i) t -= R[i + 8 * j] * R[i + 8 * c];
-      R[j + 8 * c] = t / d;
+#pragma unroll
+    for (int i = 0; i < j; ++i) s -= R[i][j] * R[i][j];
+    ok = ok && gjj > 0.0 && s >= gate * gjj;
+    const double d = sqrt(fabs(s));
+    R[j][j] = d;
+#pragma unroll
+    for (int c = j + 1; c < K; ++c) {
+      double t = g[c * (c + 1) / 2 + j];
+#pragma unroll
+      for (int i = 0; i < j; ++i) t -= R[i][j] * R[i][c];
+      R[j][c] = t / d;
     }
   }
+  if (!ok) {
+    st->gram_skip = 1;
+    return;
+  }
   // T = R^{-1}
-  for (int c = 0; c < k; ++c) {
-    T[c + 8 * c] = 1.0 / R[c + 8 * c];
+#pragma unroll
+  for (int c = 0; c < K; ++c) {
+    T[c][c] = 1.0 / R[c][c];
+#pragma unroll
     for (int i = c - 1; i >= 0; --i) {
       double t = 0.0;
-      for (int m = i + 1; m <= c; ++m) t += R[i + 8 * m] * T[m + 8 * c];
-      T[i + 8 * c] = -t / R[i + 8 * i];
+#pragma unroll
+      for (int m = i + 1; m <= c; ++m) t += R[i][m] * T[m][c];
+      T[i][c] = -t / R[i][i];
     }
   }
   double *Tout = w + (stage == 1 ? 0 : 256);
-  for (int c = 0; c < k; ++c)
-    for (int i = 0; i <= c; ++i) Tout[i + 16 * c] = T[i + 8 * c];
+#pragma unroll
+  for (int c = 0; c < K; ++c)
+#pragma unroll
+    for (int i = 0; i <= c; ++i) Tout[i + 16 * c] = T[i][c];
   if (stage == 1) {
-    for (int c = 0; c < k; ++c)
-      for (int i = 0; i <= c; ++i) w[512 + i + 16 * c] = R[i + 8 * c];
+#pragma unroll
+    for (int c = 0; c < K; ++c)
+#pragma unroll
+      for (int i = 0; i <= c; ++i) w[512 + i + 16 * c] = R[i][c];
   } else {
     // B = R2 R1: the reference's B (projection coefficients above the diagonal, the norms on it)
-    for (int c = 0; c < k; ++c)
+    double R1[K][K];
+#pragma unroll
+    for (int c = 0; c < K; ++c)
+#pragma unroll
+      for (int i = 0; i <= c; ++i) R1[i][c] = w[512 + i + 16 * c];
+#pragma unroll
+    for (int c = 0; c < K; ++c)
+#pragma unroll
       for (int i = 0; i <= c; ++i) {
         double t = 0.0;
-        for (int m = i; m <= c; ++m) t += R[i + 8 * m] * w[512 + m + 16 * c];
+#pragma unroll
+        for (int m = i; m <= c; ++m) t += R[i][m] * R1[m][c];
         st->B[i + 16 * c] = t;
       }
   }
@@ -1745,8 +1771,16 @@ void launch_fbg_b(hipStream_t s, MvDesc X, int k, int nrows, const IcgsState *st
 
 void launch_fbg_chol(hipStream_t s, const double *partial, int nblocks, int k, int stage, IcgsState *st, double *w,
                      double gate, double *sums) {
-  if (k < 2 || k > 8) throw Error(MIGMRES_EINVAL, "fbg_chol: 2 <= k <= 8");
-  k_fbg_chol<<<1, 256, 0, s>>>(partial, nblocks, k, stage, st, w, gate, sums);
+  switch (k) {
+#define FC_CASE(K)                                                                   \
+  case K:                                                                            \
+    k_fbg_chol<K><<<1, 256, 0, s>>>(partial, nblocks, stage, st, w, gate, sums);     \
+    break;
+    FBG_CASES(FC_CASE)
+#undef FC_CASE
+    default:
+      throw Error(MIGMRES_EINVAL, "fbg_chol: 2 <= k <= 8");
+  }
   LAUNCH_CHECK_();
 }
 
