@@ -4,17 +4,25 @@
 Workload (BASELINE.json configs[1]): Galeri 3-D 7-point Laplacian n = 256^3 (fp64),
 k = 8 right-hand sides, Belos BlockGmresSolMgr with "Block Size" 8, "Num Blocks" 25,
 "Orthogonalization" "ICGS", fixed-work mode ("Convergence Tolerance" 0, so every run does
-exactly --steps block iterations, restarting every 25).  X0 = 0, B = A * Xexact with
+exactly `steps` block iterations, restarting every 25).  X0 = 0, B = A * Xexact with
 Xexact from Epetra's MINSTD stream seeded with 1 (synthetic data, generated on device).
 
-A "step" is one block-Arnoldi iteration (SpMM x k + ICGS + least-squares update).
-With N GPUs (torchrun, one process per GPU) the SAME matrix is 1-D row-partitioned over
-the ranks (strong scaling): halo exchange and inner-product reductions run over RCCL.
+A "step" is one block-Arnoldi iteration (SpMM x k + ICGS + least-squares update).  --steps
+is rounded up to whole restart cycles (the line's "steps" is the count timed).
+`--gpus N` starts N rank processes (one per GPU) unless torchrun already did; the SAME
+matrix is 1-D row-partitioned over the ranks (strong scaling): halo exchange and
+inner-product reductions run over RCCL.
 
 Output: ONE JSON line on rank 0 with the contract fields plus
+  hbm           the metric's achieved HBM GB/s: algorithmic bytes of the kernels that ran
+                (library tally) / timed wall time, per GPU
   roofline      dominant kernel's algorithmic bytes per launch / mean launch time (HIP
-                events inside the library, same stream) against the 8 TB/s HBM peak
-  cpu_baseline  the numpy oracle (oracle/) timed on this host on a bounded sample
+                events inside the library, same stream) against the 8 TB/s HBM peak;
+                traffic = PMC traffic/algorithmic ratio (profiles/pmc_summary.json) x bytes
+  reference_equivalent  SURVEY 8(d)'s reference-algorithm byte model / wall time (labelled,
+                not achieved traffic)
+  cpu_baseline  the CPU restatement timed on this host on a bounded sample
+  ranks         (N > 1) per-rank halo / all-reduce device milliseconds
 """
 
 import argparse
@@ -43,44 +51,69 @@ def iteration_bytes_model(n, nnz, k, nb, iters):
     return tot
 
 
-def cpu_baseline(k, nb, seconds):
-    """Time the numpy oracle (oracle/, kind "port") on a bounded sample: the same solver
-    (ICGS, Block Size k, Num Blocks nb, tol 0) on a 64^3 Laplacian for one restart cycle,
-    then scale per-iteration time by the row count (the per-row work is the same) to the
-    256^3 workload's iterations/s."""
-    from oracle import belos as ob, epetra as oe
-    m = 64
-    n = m ** 3
-    A = oe.DistCrs(lambda f, c: oe.laplace3d_rows(m, m, m, f, c), n, 1)
-    Xex, _ = oe.epetra_random_mv(1, n, k)
-    B = A.apply(Xex)
-    iters = nb
-    t0 = time.perf_counter()
-    ob.solve(A.apply, B, {"Block Size": k, "Num Blocks": nb, "Maximum Iterations": iters,
-                          "Maximum Restarts": 1000, "Convergence Tolerance": 0.0,
-                          "Orthogonalization": "ICGS"})
-    t = time.perf_counter() - t0
-    threads = int(os.environ.get("OPENBLAS_NUM_THREADS", os.environ.get("OMP_NUM_THREADS", os.cpu_count())))
-    scale = (256 ** 3) / n
-    return {"value": iters / (t * scale), "unit": "iterations/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/belos.py on 64^3 (k={k}, Num Blocks {nb}, ICGS, tol 0): {iters} iterations "
-                      f"in {t:.2f} s, scaled by 256^3/64^3 rows to the 256^3 workload"}
+def cpu_baseline(k, nb, m, iters):
+    """The reference algorithm on this host's CPU cores (cpu_baseline.kind "port"): the C/OpenMP
+    restatement oracle/cport/bgmres.c (validated against the numpy oracle, tests/test_cport.py)
+    runs the benchmark's own workload -- Laplace3D m^3, k RHS, Block GMRES ICGS, Num Blocks nb,
+    tol 0 -- for `iters` block iterations (one whole restart cycle by default) with
+    OMP_NUM_THREADS threads.  With m < 256 the rate is scaled by rows (m^3 / 256^3) and says so."""
+    import ctypes as C
+    so = os.path.join(ROOT, "oracle", "_ref", "libcport.so")
+    lib = C.CDLL(so)
+    secs = (C.c_double * 2)()
+    nh = C.c_int()
+    rc = lib.cport_block_gmres_laplace3d(m, k, nb, iters, 1, None, C.byref(nh), None, secs)
+    if rc != 0:
+        return {"value": None, "error": f"cport returned {rc}"}
+    scale = (m ** 3) / (256 ** 3)
+    val = iters / secs[0] * scale
+    sample = (f"oracle/cport/bgmres.c (C/OpenMP restatement of the reference Block GMRES + ICGS) on Laplace3D "
+              f"{m}^3, k={k}, Num Blocks {nb}, tol 0: {iters} block iterations in {secs[0]:.2f} s")
+    if m != 256:
+        sample += f", scaled by {m}^3/256^3 rows to the 256^3 workload"
+    return {"value": val, "unit": "iterations/s", "cores": int(secs[1]), "kind": "port", "sample": sample}
 
 
-def pmc_traffic(kernel_class, world):
-    """Per-launch HBM traffic of `kernel_class` from the committed rocprofv3 PMC summary
-    (profiles/pmc_summary.json, made by tools/pmc_summary.py from separate FETCH_SIZE and
-    WRITE_SIZE passes of this bench command, gfx950 corrections per MI355X_MICROARCH.md).
-    None when no summary for this configuration exists."""
+def pmc_ratio(kernel_class, world):
+    """HBM traffic / algorithmic bytes of `kernel_class`, from the committed rocprofv3 PMC
+    summary (profiles/pmc_summary.json, made by tools/pmc_summary.py from separate FETCH_SIZE
+    and WRITE_SIZE passes of this bench command with the gfx950 corrections of
+    MI355X_MICROARCH.md, divided by the algorithmic bytes per launch of the same run).  The
+    ratio does not depend on --steps; the bench multiplies it by this run's bytes per launch.
+    None when no summary exists."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     if world != 1 or not os.path.exists(path):
         return None
     try:
-        summ = json.load(open(path))
-        ent = summ["kernels"].get(kernel_class)
-        return None if ent is None else ent["traffic_bytes_per_launch"]
+        ent = json.load(open(path))["kernels"].get(kernel_class)
+        return None if ent is None else ent.get("ratio")
     except Exception:
         return None
+
+
+def spawn_ranks(n, argv, port=None):
+    """`bench.py --gpus N` without a torchrun environment: start N rank processes of this
+    script (one per GPU, RANK = LOCAL_RANK = i, WORLD_SIZE = N, MASTER_ADDR 127.0.0.1) as
+    children, before anything in this process touches the GPU, and return the first non-zero
+    exit code (0 when every rank succeeded).  Rank 0 prints the JSON line."""
+    import socket
+    import subprocess
+    if port is None:
+        sk = socket.socket()
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+        sk.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(argv, env=env))
+    rc = 0
+    for p in procs:
+        c = p.wait()
+        if c != 0 and rc == 0:
+            rc = c
+    return rc
 
 
 def main():
@@ -93,6 +126,8 @@ def main():
     ap.add_argument("--nb", type=int, default=25)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--cpu-nx", type=int, default=256, help="cpu_baseline sample size (m^3 rows)")
+    ap.add_argument("--cpu-iters", type=int, default=0, help="cpu_baseline block iterations (0: one cycle)")
     # secondary workloads; the defaults are the headline configuration
     ap.add_argument("--solver", default="BLOCK GMRES", choices=["BLOCK GMRES", "FLEXIBLE GMRES", "GMRES"])
     ap.add_argument("--matrix", default="Laplace3D", choices=["Laplace3D", "Brick3D"])
@@ -104,7 +139,11 @@ def main():
     ap.add_argument("--ortho", default="ICGS", choices=["ICGS", "DGKS"])
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
@@ -138,6 +177,11 @@ def main():
     nnz_local = A.nnz_local
     nnz_total = int(comm.sum_all(np.array([float(nnz_local)]))[0])
 
+    # Time whole restart cycles: the cost of a block iteration grows with its position in the
+    # cycle (L = (j+1) k basis vectors to project against), so a partial cycle would flatter
+    # the rate.  --steps is rounded up to a multiple of Num Blocks; "steps" reports the count run.
+    steps = -(-args.steps // nb) * nb
+
     def run(iters):
         X.put_scalar(0.0)
         lp = ta.LinearProblem(A, X, B)
@@ -160,7 +204,7 @@ def main():
     comm.sync()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    sm = run(args.steps)
+    sm = run(steps)
     comm.sync()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
@@ -177,7 +221,7 @@ def main():
     if not args.no_profile:
         import ctypes as C
         call("migmres_ctx_profile", comm.h, 1)
-        run(args.steps)
+        run(steps)
         nk = 32  # more than the library's kernel classes; unused slots read back as 0
         ms, by, cnt = (C.c_double * nk)(), (C.c_double * nk)(), (C.c_longlong * nk)()
         call("migmres_ctx_profile_read", comm.h, ms, by, cnt, nk)
@@ -186,8 +230,8 @@ def main():
             if cnt[i]:
                 kstats[lib.migmres_kernel_class_name(i).decode()] = dict(ms=ms[i], bytes=by[i], launches=cnt[i])
 
-    value = args.steps / elapsed
-    model_bytes = iteration_bytes_model(n, nnz_total, k, nb, args.steps)
+    value = steps / elapsed
+    model_bytes = iteration_bytes_model(n, nnz_total, k, nb, steps)
     headline = (args.solver == "BLOCK GMRES" and args.matrix == "Laplace3D" and args.prec == "none"
                 and args.ortho == "ICGS" and not args.matrix_file and nx == 256 and k == 8 and nb == 25)
     mname = os.path.basename(args.matrix_file) if args.matrix_file else f"{args.matrix} n={nx}^3"
@@ -198,33 +242,61 @@ def main():
           if args.prec != "none" else
           f"{mname} fp64, k={k} RHS, {args.solver} Num Blocks {nb}, {args.ortho}, fixed work (tol 0)")
     out = {
-        "metric": METRIC, "value": value, "unit": "iterations/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps, "higher_is_better": True,
+        "metric": METRIC, "value": value, "unit": "iterations/s", "n_gpus": world, "steps": steps,
+        "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / steps, "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "f64",
         "data": (f"{mname} from file, " if args.matrix_file else "synthetic (Galeri " + args.matrix + ", ")
                 + "Xexact = Epetra MINSTD stream seed 1, B = A*Xexact)",
         "config": {"workload": wl, "n_global": n, "nnz": nnz_total, "k": k,
                    "num_blocks": nb, "parallelism": f"row1d{world}"},
-        "hbm_model": None if not headline else {"bytes_per_iteration": model_bytes / args.steps,
-                      "achieved_GBps": model_bytes / elapsed / 1e9 / world,
-                      "frac_of_peak_per_gpu": model_bytes / elapsed / 1e9 / world / HBM_PEAK_GBPS},
-        "solver_timers_s": timers,
     }
+    if steps != args.steps:
+        out["steps_requested"] = args.steps
+    out["solver_timers_s"] = timers
+    comm_cls = ("halo", "allreduce")
     if kstats:
-        dom = max(kstats, key=lambda s: kstats[s]["ms"])
+        # The metric's "achieved HBM GB/s": the algorithmic bytes the kernels that ran move
+        # (per-class byte counts tallied by the library), summed over the
+        # profiled solve (same iterations as the timed one) / the timed solve's wall time.
+        alg = sum(v["bytes"] for kn, v in kstats.items() if kn not in comm_cls)
+        if world > 1:
+            t = torch.tensor([alg], dtype=torch.float64)
+            dist.all_reduce(t)
+            alg = float(t.item())
+        gbps = alg / elapsed / 1e9 / world
+        out["hbm"] = {"achieved_GBps_per_gpu": gbps, "frac_of_peak": gbps / HBM_PEAK_GBPS,
+                      "algorithmic_bytes_per_iteration": alg / steps,
+                      "source": "per-kernel algorithmic bytes of the kernels that ran / timed wall time"}
+        dom = max((kn for kn in kstats if kn not in comm_cls), key=lambda s: kstats[s]["ms"])
         st = kstats[dom]
         per_launch_bytes = st["bytes"] / st["launches"]
         per_launch_s = st["ms"] / 1e3 / st["launches"]
         ach = per_launch_bytes / per_launch_s / 1e9
-        traffic = pmc_traffic(dom, world) if headline else None
+        ratio = pmc_ratio(dom, world) if headline else None
         out["roofline"] = {"kernel": dom, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                           "frac": ach / HBM_PEAK_GBPS, "traffic": traffic,
+                           "frac": ach / HBM_PEAK_GBPS,
+                           "traffic": None if ratio is None else ratio * per_launch_bytes,
+                           "traffic_ratio_pmc": ratio,
                            "bytes_per_launch": per_launch_bytes, "mean_launch_us": per_launch_s * 1e6}
         out["kernels"] = {kname: dict(ms=v["ms"], launches=v["launches"],
                                       GBps=v["bytes"] / (v["ms"] / 1e3) / 1e9 if v["ms"] > 0 else None)
                           for kname, v in kstats.items()}
+    if headline:
+        # SURVEY.md 8(d)'s model of the REFERENCE algorithm's traffic (column-by-column
+        # findBasis, unfused updates) over the same wall time: a reference-equivalent rate,
+        # not bytes this implementation moved (it can exceed the HBM peak).
+        out["reference_equivalent"] = {"bytes_per_iteration": model_bytes / steps,
+                                       "GBps_per_gpu": model_bytes / elapsed / 1e9 / world}
+    if world > 1:
+        mine = {"rank": rank, "comm_host_s": timers.get("comm"),
+                "halo_ms": kstats.get("halo", {}).get("ms"), "halo_launches": kstats.get("halo", {}).get("launches"),
+                "allreduce_ms": kstats.get("allreduce", {}).get("ms"),
+                "allreduce_launches": kstats.get("allreduce", {}).get("launches")}
+        allr = [None] * world
+        dist.all_gather_object(allr, mine)
+        out["ranks"] = allr
     if rank == 0 and world == 1 and not args.no_cpu_baseline and headline:
-        out["cpu_baseline"] = cpu_baseline(k, nb, 20)
+        out["cpu_baseline"] = cpu_baseline(k, nb, args.cpu_nx, args.cpu_iters if args.cpu_iters else nb)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -4,8 +4,8 @@ Each rank builds its plan with the library's host plan code (the C ABI used by
 crs_create: uniform map, Epetra column map, remote list, local CRS), runs the same
 request protocol crs_create runs over RCCL (every rank sends each owner the GIDs it
 needs, in its own order; owners answer in requester order) to get the export lists, then
-performs the halo exchange the way crs_apply does (pack per column, one message per
-neighbour and column) and the local CSR row sums.  The result must be bit-identical to the
+performs the halo exchange the way crs_apply does (pack in the [neighbour][column][count]
+layout, one message per neighbour, unpack to the ghost block) and the local CSR row sums.  The result must be bit-identical to the
 oracle's emulation of Epetra_CrsMatrix::Multiply on the same partition, and the
 distributed dot products (all-reduce of rank partials) must match.
 """
@@ -79,24 +79,29 @@ def _worker(rank, world, port, case, q):
         Xg, _ = oe.epetra_random_mv(5, n, k)
         Xloc = Xg[first:first + nloc]
         n_export, n_remote = len(export_lids), len(rg)
-        send = np.zeros((k, max(n_export, 1)))
-        for c in range(k):
-            send[c, :n_export] = Xloc[export_lids, c]
-        ghost = np.zeros((k, max(n_remote, 1)))
-        reqs = []
+        # exchange layout of crs_apply: [neighbour][column][count], one message per neighbour
+        send = np.zeros(max(n_export * k, 1))
         for (p, off, cnt) in send_nbrs:
             for c in range(k):
-                reqs.append(dist.isend(torch.from_numpy(np.ascontiguousarray(send[c, off:off + cnt])), p))
+                send[off * k + c * cnt: off * k + (c + 1) * cnt] = Xloc[export_lids[off:off + cnt], c]
+        recv = np.zeros(max(n_remote * k, 1))
+        reqs = []
+        for (p, off, cnt) in send_nbrs:
+            reqs.append(dist.isend(torch.from_numpy(np.ascontiguousarray(send[off * k:(off + cnt) * k])), p))
         bufs = []
         for (p, off, cnt) in recv_nbrs:
-            for c in range(k):
-                b = torch.zeros(cnt, dtype=torch.float64)
-                reqs.append(dist.irecv(b, p))
-                bufs.append((c, off, cnt, b))
+            b = torch.zeros(cnt * k, dtype=torch.float64)
+            reqs.append(dist.irecv(b, p))
+            bufs.append((off, cnt, b))
         for r in reqs:
             r.wait()
-        for (c, off, cnt, b) in bufs:
-            ghost[c, off:off + cnt] = b.numpy()
+        for (off, cnt, b) in bufs:
+            recv[off * k:(off + cnt) * k] = b.numpy()
+        # unpack to the ghost block [k][n_remote]
+        ghost = np.zeros((k, max(n_remote, 1)))
+        for (p, off, cnt) in recv_nbrs:
+            for c in range(k):
+                ghost[c, off:off + cnt] = recv[off * k + c * cnt: off * k + (c + 1) * cnt]
 
         # X-space indices as crs_create builds them: owned -> row id, remote -> n_local + slot
         cm = plan["colmap"]

@@ -6,7 +6,13 @@ reports half of those).  Template instantiations of one kernel (k_nn_tn_w<32, 7,
 are pooled into their bench class: traffic per launch = total corrected bytes / launches,
 the same averaging bench.py uses for the achieved rate.
 
-usage: python tools/pmc_summary.py FETCH.csv WRITE.csv STATS.csv OUT.json
+With the bench line of the same command (BENCH.json, optional) each class also gets
+`ratio` = PMC traffic per launch / algorithmic bytes per launch (the bench's per-class byte
+tally), which bench.py multiplies by its own bytes per launch for roofline.traffic.  The PMC
+run must cover whole restart cycles (as bench.py's steps do) so both averages are taken over
+the same mix of projection widths.
+
+usage: python tools/pmc_summary.py FETCH.csv WRITE.csv STATS.csv OUT.json [BENCH.json]
 """
 import csv
 import json
@@ -37,7 +43,7 @@ def load(path, counter):
     return vals
 
 
-def main(fetch_csv, write_csv, stats_csv, out_json):
+def main(fetch_csv, write_csv, stats_csv, out_json, bench_json=None):
     fe, wr = load(fetch_csv, "FETCH_SIZE"), load(write_csv, "WRITE_SIZE")
     stats = {row["Name"]: row for row in csv.DictReader(open(stats_csv))}
     out = {"source": {"fetch": fetch_csv, "write": write_csv, "stats": stats_csv},
@@ -58,11 +64,22 @@ def main(fetch_csv, write_csv, stats_csv, out_json):
         if b in KMAP:
             pool[cls][0] += traffic * nf
             pool[cls][1] += nf
+    alg = {}
+    if bench_json:
+        line = [ln for ln in open(bench_json).read().splitlines() if ln.strip().startswith("{")][-1]
+        b = json.loads(line)
+        out["source"]["bench"] = bench_json
+        for cls, v in b.get("kernels", {}).items():
+            if v.get("GBps") and v.get("launches"):
+                alg[cls] = v["GBps"] * 1e9 * v["ms"] / 1e3 / v["launches"]
     for cls, (tot, n) in pool.items():
         out["kernels"][cls] = {"traffic_bytes_per_launch": tot / max(n, 1), "dispatches": n}
+        if cls in alg:
+            out["kernels"][cls]["algorithmic_bytes_per_launch"] = alg[cls]
+            out["kernels"][cls]["ratio"] = tot / max(n, 1) / alg[cls]
     json.dump(out, open(out_json, "w"), indent=1)
     print(json.dumps(out["kernels"], indent=1))
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:5])
+    main(*sys.argv[1:6])

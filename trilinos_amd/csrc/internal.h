@@ -116,7 +116,10 @@ void launch_diag_inv(hipStream_t s, const int *rowptr, const int *cols, const do
                      double *dinv);
 void launch_jacobi(hipStream_t s, MvDesc X, MvDesc Y, const double *dinv, double omega, int nrows,
                    bool accumulate);
-// send[c*count + i] = X[lids[i], c]
-void launch_pack(hipStream_t s, MvDesc X, const int *lids, int count, double *send, int k);
+// Import exchange layout [neighbour][column][count] (grp[i] = (offset, count) of entry i's
+// neighbour group): send[off*k + c*cnt + i-off] = X[lids[i], c]; ghost[c*ldg + i] = recv[...].
+void launch_pack(hipStream_t s, MvDesc X, const int *lids, const int2 *grp, int count, double *send, int k);
+void launch_unpack(hipStream_t s, const double *recv, const int2 *grp, int count, int k, double *ghost,
+                   long long ldg);
 
 }  // namespace migmres

@@ -819,11 +819,28 @@ __global__ __launch_bounds__(256) void k_random(MvDesc Y, int nrows, long long f
   colp(Y, c)[r] = 2.0 * (x / 2147483647.0) - 1.0;
 }
 
-__global__ __launch_bounds__(256) void k_pack(MvDesc X, const int *__restrict__ lids, int count,
+// Import pack / unpack in the exchange layout [neighbour][column][count]: one contiguous
+// message per neighbour and apply (Epetra packs row-interleaved per export LID,
+// Epetra_MultiVector.cpp:778-783; one message per peer either way).  grp[i] = (offset,
+// count) of entry i's neighbour group in the export (or remote) list; entry i of column c
+// sits at offset*k + c*count + (i - offset).
+__global__ __launch_bounds__(256) void k_pack(MvDesc X, const int *__restrict__ lids,
+                                              const int2 *__restrict__ grp, int count, int k,
                                               double *__restrict__ send) {
   const int c = blockIdx.y;
   const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i < count) send[(long long)c * count + i] = colp(X, c)[lids[i]];
+  if (i >= count) return;
+  const int2 g = grp[i];
+  send[(long long)g.x * k + (long long)c * g.y + (i - g.x)] = colp(X, c)[lids[i]];
+}
+__global__ __launch_bounds__(256) void k_unpack(const double *__restrict__ recv,
+                                                const int2 *__restrict__ grp, int count, int k,
+                                                double *__restrict__ ghost, long long ldg) {
+  const int c = blockIdx.y;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= count) return;
+  const int2 g = grp[i];
+  ghost[(long long)c * ldg + i] = recv[(long long)g.x * k + (long long)c * g.y + (i - g.x)];
 }
 
 // Point-Jacobi (Ifpack2::Relaxation "Jacobi", Ifpack2_Relaxation_def.hpp:1390-1454).
@@ -901,9 +918,15 @@ void launch_random(hipStream_t s, MvDesc Y, int nrows, long long first, long lon
   k_random<<<dim3(cdiv(nrows, 256), Y.ncols), 256, 0, s>>>(Y, nrows, first, n_global, seed);
   LAUNCH_CHECK();
 }
-void launch_pack(hipStream_t s, MvDesc X, const int *lids, int count, double *send, int k) {
+void launch_pack(hipStream_t s, MvDesc X, const int *lids, const int2 *grp, int count, double *send, int k) {
   if (count <= 0 || k <= 0) return;
-  k_pack<<<dim3(cdiv(count, 256), k), 256, 0, s>>>(X, lids, count, send);
+  k_pack<<<dim3(cdiv(count, 256), k), 256, 0, s>>>(X, lids, grp, count, k, send);
+  LAUNCH_CHECK();
+}
+void launch_unpack(hipStream_t s, const double *recv, const int2 *grp, int count, int k, double *ghost,
+                   long long ldg) {
+  if (count <= 0 || k <= 0) return;
+  k_unpack<<<dim3(cdiv(count, 256), k), 256, 0, s>>>(recv, grp, count, k, ghost, ldg);
   LAUNCH_CHECK();
 }
 

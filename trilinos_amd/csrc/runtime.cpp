@@ -177,7 +177,10 @@ void migmres_ctx::allreduce(double *d, size_t n, bool max) {
   if (loop) {
     loop_allreduce(this, d, n, max);
   } else {
-    MIG_NCCL(ncclAllReduce(d, d, n, ncclDouble, max ? ncclMax : ncclSum, comm, stream));
+    {
+      ProfScope ps(this, K_ALLREDUCE, 8.0 * n);
+      MIG_NCCL(ncclAllReduce(d, d, n, ncclDouble, max ? ncclMax : ncclSum, comm, stream));
+    }
     MIG_HIP(hipStreamSynchronize(stream));
   }
   comm_seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -185,7 +188,8 @@ void migmres_ctx::allreduce(double *d, size_t n, bool max) {
 
 const char *kKernelClassNames[K_NUM_CLASSES] = {"spmm", "gemm_tn", "reduce", "gemm_nn", "coldot",
                                                 "axpby", "scale", "fill", "copy", "random", "pack",
-                                                "findbasis", "gemm_nn_dot", "nn_tn"};
+                                                "findbasis", "gemm_nn_dot", "nn_tn", "halo",
+                                                "allreduce"};
 
 hipEvent_t migmres_ctx::get_event() {
   if (!event_pool.empty()) {
@@ -203,6 +207,7 @@ void migmres_ctx::prof_collect() {
   MIG_HIP(hipStreamSynchronize(stream));
   for (auto &p : pending) {
     float ms = 0.f;
+    MIG_HIP(hipEventSynchronize(p.b));
     MIG_HIP(hipEventElapsedTime(&ms, p.a, p.b));
     prof_ms[p.cls] += ms;
     prof_bytes[p.cls] += p.bytes;
@@ -213,16 +218,17 @@ void migmres_ctx::prof_collect() {
   pending.clear();
 }
 
-ProfScope::ProfScope(migmres_ctx *ctx, int k, double by) : c(ctx), cls(k), bytes(by) {
+ProfScope::ProfScope(migmres_ctx *ctx, int k, double by, hipStream_t stream)
+    : c(ctx), cls(k), bytes(by), s(stream ? stream : ctx->stream) {
   if (!c->prof_on) return;
   a = c->get_event();
   b = c->get_event();
-  MIG_HIP(hipEventRecord(a, c->stream));
+  MIG_HIP(hipEventRecord(a, s));
 }
 
 ProfScope::~ProfScope() {
   if (!c->prof_on || !a) return;
-  hipEventRecord(b, c->stream);
+  hipEventRecord(b, s);
   c->pending.push_back({cls, bytes, a, b});
   if (c->pending.size() > 2048) {
     try {
@@ -298,6 +304,7 @@ void migmres_ctx::allreduce_async(double *d, size_t n) {
     loop_allreduce(this, d, n, false);
     return;
   }
+  ProfScope ps(this, K_ALLREDUCE, 8.0 * n);
   MIG_NCCL(ncclAllReduce(d, d, n, ncclDouble, ncclSum, comm, stream));
 }
 
@@ -649,6 +656,8 @@ void mv_assign(const migmres_mv &A, migmres_mv &Y) {
 migmres_crs::~migmres_crs() {
   for (void *p : {(void *)d_soff, (void *)d_slen, (void *)d_scol, (void *)d_sval})
     if (p) hipFree(p);
+  for (void *p : {(void *)d_export_grp, (void *)d_remote_grp, (void *)d_recv})
+    if (p) hipFree(p);
   for (void *p : {(void *)d_rowptr, (void *)d_cols, (void *)d_export, (void *)d_vals, (void *)d_send,
                   (void *)d_ghost, (void *)d_psv, (void *)d_psk, (void *)d_psm, (void *)d_sel_int,
                   (void *)d_sel_bnd})
@@ -814,11 +823,20 @@ migmres_crs *crs_create(migmres_ctx *ctx, long long n_global, long long first, i
       if (!sel_bnd.empty())
         MIG_HIP(hipMemcpy(A->d_sel_bnd, sel_bnd.data(), sizeof(int) * sel_bnd.size(), hipMemcpyHostToDevice));
     }
+    auto upload_groups = [](const std::vector<migmres_crs::Nbr> &nbrs, size_t n, int2 **out) {
+      std::vector<int2> g(n);
+      for (auto &nb : nbrs)
+        for (int i = 0; i < nb.count; ++i) g[(size_t)(nb.offset + i)] = make_int2(nb.offset, nb.count);
+      MIG_HIP(hipMalloc(out, sizeof(int2) * n));
+      MIG_HIP(hipMemcpy(*out, g.data(), sizeof(int2) * n, hipMemcpyHostToDevice));
+    };
     if (!A->export_lids.empty()) {
       MIG_HIP(hipMalloc(&A->d_export, sizeof(int) * A->export_lids.size()));
       MIG_HIP(hipMemcpy(A->d_export, A->export_lids.data(), sizeof(int) * A->export_lids.size(),
                         hipMemcpyHostToDevice));
+      upload_groups(A->send_nbrs, A->export_lids.size(), &A->d_export_grp);
     }
+    if (n_remote > 0) upload_groups(A->recv_nbrs, (size_t)n_remote, &A->d_remote_grp);
   } catch (...) {
     delete A;
     throw;
@@ -849,10 +867,11 @@ void crs_apply(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, double alpha,
     if (k > A.halo_k) {
       MIG_HIP(hipStreamSynchronize(c->stream));
       MIG_HIP(hipStreamSynchronize(c->halo_stream));
-      if (A.d_send) hipFree(A.d_send);
-      if (A.d_ghost) hipFree(A.d_ghost);
-      A.d_send = A.d_ghost = nullptr;
+      for (double *p : {A.d_send, A.d_recv, A.d_ghost})
+        if (p) hipFree(p);
+      A.d_send = A.d_recv = A.d_ghost = nullptr;
       MIG_HIP(hipMalloc(&A.d_send, sizeof(double) * ((size_t)n_export * k + 1)));
+      MIG_HIP(hipMalloc(&A.d_recv, sizeof(double) * ((size_t)n_remote * k + 1)));
       A.ldg = (n_remote + 1) & ~1LL;
       MIG_HIP(hipMalloc(&A.d_ghost, sizeof(double) * ((size_t)A.ldg * k + 2)));
       MIG_HIP(hipMemset(A.d_ghost, 0, sizeof(double) * ((size_t)A.ldg * k + 2)));
@@ -860,19 +879,22 @@ void crs_apply(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, double alpha,
     }
     // Import on the halo stream (Epetra_Import through Epetra_MpiDistributor::Do), ordered
     // after everything already queued on the context stream (X is ready, the previous
-    // apply's boundary rows have read the ghost block).
+    // apply's boundary rows have read the ghost block).  One message of k*count doubles per
+    // neighbour each way (Epetra_MpiDistributor::DoPosts, Epetra_MpiDistributor.cpp:781-947).
     auto t0 = std::chrono::steady_clock::now();
     MIG_HIP(hipEventRecord(c->ev_main, c->stream));
     MIG_HIP(hipStreamWaitEvent(c->halo_stream, c->ev_main, 0));
-    launch_pack(c->halo_stream, X.desc(), A.d_export, n_export, A.d_send, k);
-    c->p2p_begin(c->halo_stream);
-    for (auto &nb : A.send_nbrs)
-      for (int col = 0; col < k; ++col)
-        c->p2p_send(A.d_send + (size_t)col * n_export + nb.offset, sizeof(double) * nb.count, nb.pid);
-    for (auto &nb : A.recv_nbrs)
-      for (int col = 0; col < k; ++col)
-        c->p2p_recv(A.d_ghost + (size_t)col * A.ldg + nb.offset, sizeof(double) * nb.count, nb.pid);
-    c->p2p_end();
+    {
+      ProfScope hs(c, K_HALO, 8.0 * k * ((double)n_export + n_remote), c->halo_stream);
+      launch_pack(c->halo_stream, X.desc(), A.d_export, A.d_export_grp, n_export, A.d_send, k);
+      c->p2p_begin(c->halo_stream);
+      for (auto &nb : A.send_nbrs)
+        c->p2p_send(A.d_send + (size_t)nb.offset * k, sizeof(double) * nb.count * k, nb.pid);
+      for (auto &nb : A.recv_nbrs)
+        c->p2p_recv(A.d_recv + (size_t)nb.offset * k, sizeof(double) * nb.count * k, nb.pid);
+      c->p2p_end();
+      launch_unpack(c->halo_stream, A.d_recv, A.d_remote_grp, n_remote, k, A.d_ghost, A.ldg);
+    }
     MIG_HIP(hipEventRecord(c->ev_halo, c->halo_stream));
     c->comm_seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }

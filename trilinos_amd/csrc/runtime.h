@@ -12,8 +12,11 @@
 #include "plan.h"
 
 // Per-kernel-class profiling with HIP events on the context stream (bench.py roofline).
+// K_HALO (halo stream: pack, exchange, unpack) and K_ALLREDUCE (RCCL all-reduce on the
+// context stream) are communication classes: their bytes are the message payload.
 enum KernelClass { K_SPMM = 0, K_GEMM_TN, K_REDUCE, K_GEMM_NN, K_COLDOT, K_AXPBY, K_SCALE, K_FILL,
-                   K_COPY, K_RANDOM, K_PACK, K_FB, K_GEMM_NN_DOT, K_NN_TN, K_NUM_CLASSES };
+                   K_COPY, K_RANDOM, K_PACK, K_FB, K_GEMM_NN_DOT, K_NN_TN, K_HALO, K_ALLREDUCE,
+                   K_NUM_CLASSES };
 extern const char *kKernelClassNames[K_NUM_CLASSES];
 
 struct migmres_ctx;
@@ -25,7 +28,8 @@ struct ProfScope {
   int cls;
   double bytes;
   hipEvent_t a = nullptr, b = nullptr;
-  ProfScope(migmres_ctx *ctx, int cls, double bytes);
+  hipStream_t s = nullptr;
+  ProfScope(migmres_ctx *ctx, int cls, double bytes, hipStream_t stream = nullptr);
   ~ProfScope();
 };
 
@@ -125,6 +129,9 @@ struct migmres_crs {
   };
   std::vector<Nbr> recv_nbrs, send_nbrs;
   int *d_rowptr = nullptr, *d_cols = nullptr, *d_export = nullptr;
+  // (offset, count) of each export / remote entry's neighbour group: the exchange buffers are
+  // laid out [neighbour][column][count], one message per neighbour (launch_pack / unpack)
+  int2 *d_export_grp = nullptr, *d_remote_grp = nullptr;
   double *d_vals = nullptr;  // padded by 8 zero entries (row-pair kernel reads 8 per row)
   // row-pair gather plan (k_spmm_pair); null when the matrix does not fit it
   double *d_psv = nullptr;  // SELL-64 layout of the pair plan (make_pair_sell)
@@ -141,7 +148,7 @@ struct migmres_crs {
   // units read no ghost column and run while the halo exchange is in flight
   int *d_sel_int = nullptr, *d_sel_bnd = nullptr;
   int n_sel_int = 0, n_sel_bnd = 0;
-  double *d_send = nullptr, *d_ghost = nullptr;
+  double *d_send = nullptr, *d_recv = nullptr, *d_ghost = nullptr;
   long long ldg = 0;  // ghost block leading dimension: n_remote rounded up to even, padding zero
   int halo_k = 0;
   ~migmres_crs();
