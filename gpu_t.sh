@@ -1,4 +1,3 @@
 source ./tools_gpu_check.sh
 export TMPDIR=/tmp
-step 600 pytest_gpu.log python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
-step 600 bench.log python bench.py
+step 1100 pytest_all.log python -u -m pytest tests -m gpu -v -s --timeout 400 --timeout-method thread --durations=25

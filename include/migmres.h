@@ -119,7 +119,9 @@ int migmres_crs_create(migmres_ctx *ctx, long long n_global, long long first, in
                        const long long *rowptr, const long long *gcols, const double *vals,
                        migmres_crs **out);
 /* Galeri generators built natively on the host of each rank ("Laplace2D", "Laplace3D",
- * "Brick3D" = the 27-point Xpetra Brick3D with a = 26, b..g = -1); nz ignored for 2-D. */
+ * "Brick3D" = the 27-point Xpetra Brick3D with a = 26, b..g = -1); nz ignored for 2-D.
+ * "FlanProxy" (not Galeri: a synthetic stand-in of SuiteSparse Flan_1565, 3 dofs per node of
+ * an nx x ny x nz node grid, ~73 nnz per row, scrambled numbering, nx odd) has 3 nx ny nz rows. */
 int migmres_crs_create_galeri(migmres_ctx *ctx, const char *kind, int nx, int ny, int nz,
                               migmres_crs **out);
 /* The same generator on the host only: rows [first, first+n_local) with GLOBAL columns in

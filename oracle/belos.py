@@ -40,11 +40,45 @@ class RandomSource:
         return v[:, 0].copy()
 
 
+# Summation order of the inner products (test infrastructure): "blas" is the restatement's
+# default; "reversed" sums the same products over the rows in reverse order.  Running the
+# oracle both ways measures how far rounding alone moves a solve's residual history -- the
+# yardstick for the GPU's differently ordered (blocked, MFMA) sums (tests/test_gpu_solver.py).
+SUM_ORDER = "blas"
+
+
+class summation_order:
+    """with summation_order("reversed"): ... -- the oracle's inner products in another order."""
+
+    def __init__(self, order):
+        self.order = order
+
+    def __enter__(self):
+        global SUM_ORDER
+        self.prev, SUM_ORDER = SUM_ORDER, self.order
+        return self
+
+    def __exit__(self, *exc):
+        global SUM_ORDER
+        SUM_ORDER = self.prev
+
+
+def _tn(Q, X):
+    """Q^T X (MvTransMv)."""
+    if SUM_ORDER == "reversed":
+        return Q[::-1].T @ X[::-1]
+    return Q.T @ X
+
+
 def _dot(a, b):
+    if SUM_ORDER == "reversed":
+        return float(np.dot(a[::-1], b[::-1]))
     return float(np.dot(a, b))
 
 
 def _coldots(X, Y):
+    if SUM_ORDER == "reversed":
+        return np.einsum("ij,ij->j", X[::-1], Y[::-1])
     return np.einsum("ij,ij->j", X, Y)
 
 
@@ -93,10 +127,10 @@ class ICGS:
 
     def _blk_ortho1(self, X, Q, C):
         """blkOrtho1 (BelosICGSOrthoManager.hpp:1231-1322), no mass operator."""
-        C[:] = Q.T @ X
+        C[:] = _tn(Q, X)
         X -= Q @ C
         for _ in range(1, self.steps):
-            C2 = Q.T @ X
+            C2 = _tn(Q, X)
             C += C2
             X -= Q @ C2
         return False
@@ -104,10 +138,10 @@ class ICGS:
     def _blk_ortho(self, X, Q, C):
         """blkOrtho (BelosICGSOrthoManager.hpp:1328-1445)."""
         old = _coldots(X, X)
-        C[:] = Q.T @ X
+        C[:] = _tn(Q, X)
         X -= Q @ C
         for _ in range(1, self.steps):
-            C2 = Q.T @ X
+            C2 = _tn(Q, X)
             C += C2
             X -= Q @ C2
         new = _coldots(X, X)
@@ -127,7 +161,7 @@ class ICGS:
             product = np.zeros(j)
             if j > 0:
                 for i in range(self.steps):
-                    P2 = prevX.T @ Xj
+                    P2 = _tn(prevX, Xj)
                     Xj -= prevX @ P2
                     product = P2.copy() if i == 0 else product + P2
                 new_dot = _dot(Xj, old_xj)
@@ -140,7 +174,7 @@ class ICGS:
                     old_dot = _dot(t, t)
                     for _ in range(self.steps):
                         if j > 0:
-                            pr = prevX.T @ t
+                            pr = _tn(prevX, t)
                             t -= prevX @ pr
                     new_dot = _dot(t, t)
                     if abs(new_dot) >= abs(old_dot * self.sing_tol):
@@ -171,12 +205,12 @@ class ICGS:
             old_dot = _dot(Xj, Xj)
             for Qi, Ci in zip(Qs, Cs):
                 nq = Qi.shape[1]
-                Ci[:nq, j] = Qi.T @ Xj
+                Ci[:nq, j] = _tn(Qi, Xj)
                 Xj -= Qi @ Ci[:nq, j]
             for _ in range(1, self.steps):
                 for Qi, Ci in zip(Qs, Cs):
                     nq = Qi.shape[1]
-                    C2 = Qi.T @ Xj
+                    C2 = _tn(Qi, Xj)
                     Ci[:nq, j] += C2
                     Xj -= Qi @ C2
             dep = abs(new_dot) < abs(old_dot * self.sing_tol)
@@ -189,7 +223,7 @@ class ICGS:
                 old_dot = _dot(t, t)
                 for _ in range(self.steps):
                     for Qi in Qs:
-                        pr = Qi.T @ t
+                        pr = _tn(Qi, t)
                         t -= Qi @ pr
                 new_dot = _dot(t, t)
                 if abs(new_dot) >= abs(old_dot * self.sing_tol):

@@ -18,7 +18,7 @@ import math
 
 import numpy as np
 
-from .belos import ICGS, ICGS_BLK_TOL, ICGS_SING_TOL, _dot
+from .belos import ICGS, ICGS_BLK_TOL, ICGS_SING_TOL, _dot, _tn
 
 DGKS_DEP_TOL = 1.0 / math.sqrt(2.0)   # BelosDGKSOrthoManager.hpp:546-550
 
@@ -31,11 +31,11 @@ class DGKS(ICGS):
     def _blk_ortho1(self, X, Q, C):
         """blkOrtho1 (BelosDGKSOrthoManager.hpp:1245-1321)."""
         old = _dot(X[:, 0], X[:, 0])
-        C[:] = Q.T @ X
+        C[:] = _tn(Q, X)
         X -= Q @ C
         new = _dot(X[:, 0], X[:, 0])
         if math.sqrt(abs(new)) < self.dep_tol * math.sqrt(abs(old)):
-            C2 = Q.T @ X
+            C2 = _tn(Q, X)
             C += C2
             X -= Q @ C2
         return False
@@ -53,11 +53,11 @@ class DGKS(ICGS):
                 raise ValueError("negative definiteness in inner product")
             product = np.zeros(j)
             if j > 0:
-                product = prevX.T @ Xj
+                product = _tn(prevX, Xj)
                 Xj -= prevX @ product
                 new_dot = _dot(Xj, Xj)
                 if math.sqrt(abs(new_dot)) < self.dep_tol * math.sqrt(abs(old_dot)):
-                    P2 = prevX.T @ Xj
+                    P2 = _tn(prevX, Xj)
                     product = product + P2
                     Xj -= prevX @ P2
                 new_dot = _dot(Xj, old_xj)
@@ -70,7 +70,7 @@ class DGKS(ICGS):
                     old_dot = _dot(t, t)
                     for _ in range(self.steps):
                         if j > 0:
-                            pr = prevX.T @ t
+                            pr = _tn(prevX, t)
                             t -= prevX @ pr
                     new_dot = _dot(t, t)
                     if abs(new_dot) >= abs(old_dot * self.sing_tol):
@@ -99,13 +99,13 @@ class DGKS(ICGS):
             old_dot = _dot(Xj, Xj)
             for Qi, Ci in zip(Qs, Cs):
                 nq = Qi.shape[1]
-                Ci[:nq, j] = Qi.T @ Xj
+                Ci[:nq, j] = _tn(Qi, Xj)
                 Xj -= Qi @ Ci[:nq, j]
             new_dot = _dot(Xj, Xj)
             if abs(new_dot) < abs(old_dot * self.dep_tol):
                 for Qi, Ci in zip(Qs, Cs):
                     nq = Qi.shape[1]
-                    C2 = Qi.T @ Xj
+                    C2 = _tn(Qi, Xj)
                     Ci[:nq, j] += C2
                     Xj -= Qi @ C2
                 new_dot = _dot(Xj, Xj)
@@ -118,7 +118,7 @@ class DGKS(ICGS):
                 old_dot = _dot(t, t)
                 for _ in range(self.steps):
                     for Qi in Qs:
-                        pr = Qi.T @ t
+                        pr = _tn(Qi, t)
                         t -= Qi @ pr
                 new_dot = _dot(t, t)
                 if abs(new_dot) >= abs(old_dot * self.sing_tol):

@@ -70,7 +70,13 @@ def main(names=None):
         res = ob.solve(A.apply, B, params)
         R = B - A.apply(res["X"])
         rel = np.linalg.norm(R, axis=0) / np.linalg.norm(B, axis=0)
-        np.savez_compressed(os.path.join(HERE, f"{name}.npz"), history=res["history"], true_rel=rel)
+        # the same solve with the oracle's inner products summed in reverse row order: how far
+        # rounding alone moves the history (the GPU tests' bar beyond 1e-12, test_gpu_solver.py)
+        with ob.summation_order("reversed"):
+            rev = ob.solve(A.apply, B, params)
+        assert rev["iterations"] == res["iterations"] and rev["history"].shape == res["history"].shape
+        np.savez_compressed(os.path.join(HERE, f"{name}.npz"), history=res["history"], true_rel=rel,
+                            history_reversed=rev["history"])
         meta = dict(kind=kind, dims=dims, k=k, seed=seed, params=params, iterations=res["iterations"],
                     converged=bool(res["converged"]), n_apply=res["n_apply"],
                     n_explicit=res["n_explicit"], restarts=res["restarts"],

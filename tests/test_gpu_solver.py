@@ -3,10 +3,12 @@
 Parity bar (north star): identical iteration counts and solver decisions (restarts,
 explicit-residual checks, operator applies), and the implicit residual history -- the
 relative residuals ||r_j|| / ||r_0|| that the status test compares against the tolerance --
-within 1e-12 of ||r_0|| per restart cycle (1e-12 for an unrestarted run).  The two differ
-only in the floating-point summation order of the inner products; the difference grows with
-the number of restarts because each restart re-forms B - A X from the accumulated X (see
-test_long_restarted_run_drift).
+within 1e-12 (_hist_close).  Where a restarted run moves further than that, the bound is the
+algorithm's own rounding sensitivity, measured rather than assumed: the oracle re-run with
+every inner product summed in the reverse row order (oracle.belos.summation_order) must
+itself move by at least a tenth of the GPU's distance.  Restarts re-form B - A X from an X
+that carries every previous cycle's rounding, so this sensitivity grows with the number of
+restarts (test_long_restarted_run_drift).
 """
 
 import json
@@ -57,10 +59,33 @@ def _device_solve(comm, kind, dims, k, seed, params, nrhs=None):
     return sm, ret, X.download(), B.download(), Xex
 
 
-def _hist_close(h, ref, restarts=0):
-    """Histories agree within 1e-12 of ||r0|| per restart cycle (see module docstring)."""
+def _hist_close(h, ref, rerun=None):
+    """Histories within 1e-12 of ||r0||; or, when they differ by more, within ten times the
+    oracle's own summation-order drift.  `rerun` is the oracle history with reversed-order
+    inner products, or a callable returning it (oracle_rerun); it is only evaluated when
+    needed.  A rerun that changes the oracle's own decisions (history shape) marks a case
+    whose decisions are rounding-unstable: not a parity case."""
     assert h.shape == ref.shape, (h.shape, ref.shape)
-    np.testing.assert_allclose(h, ref, rtol=0, atol=HIST_ATOL * (restarts + 1))
+    d = float(np.abs(h - ref).max()) if h.size else 0.0
+    print(f"[hist] max |gpu - oracle| = {d:.3e}")
+    if d <= HIST_ATOL:
+        return
+    assert rerun is not None, f"history differs by {d:.3e} > {HIST_ATOL} and no oracle drift was measured"
+    ref2 = rerun() if callable(rerun) else rerun
+    assert ref2.shape == ref.shape, "the oracle's own decisions change with the summation order"
+    drift = float(np.abs(ref2 - ref).max())
+    print(f"[hist] oracle summation-order drift = {drift:.3e}")
+    assert d <= HIST_ATOL + 10.0 * drift, f"GPU-oracle {d:.3e} vs oracle-oracle drift {drift:.3e}"
+
+
+def oracle_rerun(fn, *args, **kw):
+    """A callable for _hist_close: the oracle call fn(*args, **kw) (returning a result dict with
+    "history") with its inner products summed in reverse row order."""
+    def run():
+        from oracle import belos as ob
+        with ob.summation_order("reversed"):
+            return fn(*args, **kw)["history"]
+    return run
 
 
 @pytest.mark.parametrize("kind,dims,k,nb,seed", [("Laplace2D", (30, 30, 1), 1, 20, 1),
@@ -82,17 +107,18 @@ def test_small_solves_match_oracle(comm, kind, dims, k, nb, seed):
     assert c["explicit_checks"] == ref["n_explicit"]
     assert c["restarts"] == ref["restarts"]
     assert c["applies"] == ref["n_apply"]
-    _hist_close(sm.residualHistory(), ref["history"], ref["restarts"])
+    _hist_close(sm.residualHistory(), ref["history"], oracle_rerun(ob.solve, Aor.apply, Aor.apply(Xex), params))
     rel = np.linalg.norm(B - Aor.apply(X), axis=0) / np.linalg.norm(B, axis=0)
     assert rel.max() <= 1e-9
 
 
 def test_long_restarted_run_drift(comm):
     """40 restarts of an 8-block cycle on a 40x25 2-D Laplacian (condition number ~600):
-    every solver decision still matches the oracle; the residual history drifts by up to
-    ~1e-11 of ||r0|| (measured 1.1e-11 on MI355X), because each restart re-forms B - A X
-    from an X that carries the accumulated rounding of all previous cycles -- hence the
-    1e-12-per-restart-cycle budget."""
+    every solver decision still matches the oracle; the residual history moves by up to
+    ~1e-11 of ||r0|| (measured 1.1e-11 on MI355X) because each restart re-forms B - A X from
+    an X that carries the accumulated rounding of all previous cycles.  The oracle moves by a
+    comparable amount when only its summation order changes: the drift is the algorithm's,
+    not the device's."""
     import trilinos_amd as ta
     from oracle import belos as ob, epetra as oe
     params = {"Block Size": 3, "Num Blocks": 8, "Maximum Iterations": 400, "Maximum Restarts": 40,
@@ -103,7 +129,10 @@ def test_long_restarted_run_drift(comm):
     ref = ob.solve(Aor.apply, Aor.apply(Xex), params)
     assert sm.getNumIters() == ref["iterations"] and sm.counters()["restarts"] == ref["restarts"] >= 30
     assert sm.counters()["explicit_checks"] == ref["n_explicit"]
-    _hist_close(sm.residualHistory(), ref["history"], ref["restarts"])
+    ref2 = oracle_rerun(ob.solve, Aor.apply, Aor.apply(Xex), params)()
+    drift = np.abs(ref2 - ref["history"]).max()
+    assert drift > 1e-13  # rounding alone moves the restarted history
+    _hist_close(sm.residualHistory(), ref["history"], ref2)
 
 
 def test_multiple_rhs_blocks(comm):
@@ -120,7 +149,7 @@ def test_multiple_rhs_blocks(comm):
         ref = ob.solve(Aor.apply, Aor.apply(Xex), params)
         assert sm.getNumIters() == ref["iterations"]
         assert sm.counters()["applies"] == ref["n_apply"]
-        _hist_close(sm.residualHistory(), ref["history"], ref["restarts"])
+        _hist_close(sm.residualHistory(), ref["history"], oracle_rerun(ob.solve, Aor.apply, Aor.apply(Xex), params))
         assert ret == ta.Converged
         rel = np.linalg.norm(B - Aor.apply(X), axis=0) / np.linalg.norm(B, axis=0)
         assert rel.max() <= 1e-8
@@ -168,7 +197,7 @@ def test_reference_pinned_runs(comm, name):
     c = sm.counters()
     assert c["applies"] == meta["n_apply"] and c["explicit_checks"] == meta["n_explicit"]
     assert c["restarts"] == meta["restarts"]
-    _hist_close(sm.residualHistory(), gold["history"], meta["restarts"])
+    _hist_close(sm.residualHistory(), gold["history"], gold["history_reversed"])
     from oracle import epetra as oe
     n, gen = _gen(meta["kind"], tuple(meta["dims"]))
     rel = np.linalg.norm(B - oe.DistCrs(gen, n, 1).apply(X), axis=0) / np.linalg.norm(B, axis=0)
@@ -217,7 +246,7 @@ def test_dependent_blocks_blkorthosing(comm):
     assert c["restarts"] == ref["restarts"] and c["applies"] == ref["n_apply"]
     assert c["explicit_checks"] == ref["n_explicit"]
     assert c["blk_ortho_sing"] == ref["blk_ortho_sing"]
-    _hist_close(sm.residualHistory(), ref["history"], ref["restarts"])
+    _hist_close(sm.residualHistory(), ref["history"])
 
 
 @pytest.mark.parametrize("kind,dims,k,nb,seed", [("Laplace3D", (16, 16, 16), 8, 6, 3),
@@ -238,7 +267,7 @@ def test_dgks_solves_match_oracle(comm, kind, dims, k, nb, seed):
     assert sm.getNumIters() == ref["iterations"]
     assert c["restarts"] == ref["restarts"] and c["applies"] == ref["n_apply"]
     assert c["explicit_checks"] == ref["n_explicit"]
-    _hist_close(sm.residualHistory(), ref["history"], ref["restarts"])
+    _hist_close(sm.residualHistory(), ref["history"], oracle_rerun(ob.solve, A.apply, A.apply(Xex), params))
 
 
 def test_dgks_orsirr1_reference_run(comm):
@@ -265,7 +294,8 @@ def test_dgks_orsirr1_reference_run(comm):
     rel = np.linalg.norm(b - Aor.apply(X.download())[:, 0]) / np.linalg.norm(b)
     assert f"{rel:.5e}" == "9.94786e-06"
     ref = ob.solve(Aor.apply, b[:, None], dict(params, Orthogonalization="DGKS"))
-    _hist_close(sm.residualHistory(), ref["history"], ref["restarts"])
+    _hist_close(sm.residualHistory(), ref["history"],
+                oracle_rerun(ob.solve, Aor.apply, b[:, None], dict(params, Orthogonalization="DGKS")))
 
 
 @pytest.mark.parametrize("env", [{"MIGMRES_FB_GRAM": "0"}, {"MIGMRES_FB_GRAM_GATE": "2"},
@@ -275,7 +305,7 @@ def test_gram_findbasis_against_column_passes(comm, monkeypatch, env):
     its pivots; the default for ICGS with 2 <= k <= 8) against the column-by-column passes
     (MIGMRES_FB_GRAM=0), against its own gate hand-back (gate 2: every block goes to the
     column passes, after the speculative SpMM has read it) and against its unfused form: the
-    same solver decisions and iteration counts, histories within 1e-12 of ||r0|| per cycle."""
+    same solver decisions and iteration counts, histories within the oracle bar."""
     params = {"Block Size": 4, "Num Blocks": 10, "Maximum Iterations": 400, "Maximum Restarts": 40,
               "Convergence Tolerance": 1e-9, "Orthogonalization": "ICGS"}
     sm, ret, X, _, _ = _device_solve(comm, "Laplace3D", (14, 13, 12), 4, 7, params)
@@ -285,5 +315,15 @@ def test_gram_findbasis_against_column_passes(comm, monkeypatch, env):
     c = sm.counters()
     assert ret2 == ret and sm2.getNumIters() == sm.getNumIters()
     assert sm2.counters() == c
-    _hist_close(sm2.residualHistory(), sm.residualHistory(), c["restarts"])
+
+    def drift():
+        from oracle import belos as ob, epetra as oe
+        n, gen = _gen("Laplace3D", (14, 13, 12))
+        Aor = oe.DistCrs(gen, n, 1)
+        Xex, _ = oe.epetra_random_mv(7, n, 4)
+        B = Aor.apply(Xex)
+        h1 = ob.solve(Aor.apply, B, params)["history"]
+        # the first GPU history shifted by the oracle's summation-order drift
+        return sm.residualHistory() + (oracle_rerun(ob.solve, Aor.apply, B, params)() - h1)
+    _hist_close(sm2.residualHistory(), sm.residualHistory(), drift)
     np.testing.assert_allclose(X2, X, rtol=0, atol=1e-8 * np.abs(X).max())

@@ -154,9 +154,84 @@ void local_crs(int n_local, const long long *rowptr, const long long *gcols, con
 // neighbours: galeri/src-epetra/Galeri_Utils.cpp:331-398); "Brick3D" is the 27-point
 // Xpetra Brick3D (galeri/src-xpetra/Galeri_XpetraMatrixTypes.hpp:533-630) with a = 26,
 // b..g = -1 and Dirichlet truncation on every face (boundary rows keep 26).
+//
+// "FlanProxy" (not a Galeri matrix): a stand-in of BASELINE config 4's SuiteSparse
+// Flan_1565 (3-D hexahedral FE model of a flange, 3 dofs per node, ~73 nnz per row), which is
+// not in this image.  Nodes on an nx x ny x nz grid, 3 dofs each; node v couples to every
+// in-range node of its 3x3x3 neighbourhood except a deterministic 1/13 of the edges
+// (symmetric: decided on the unordered pair), giving ~73 nnz per row at 81 x 81 x 80 nodes
+// (1,574,640 rows).  The node numbering is scrambled along each grid line
+// (ix -> (32 ix + 7) mod nx, nx coprime to 32) so a row's columns are irregular, as in an
+// unstructured mesh.  Off-diagonal values -(h+1)/997 with h a hash of (row, column); the
+// diagonal is 1 + the sum of the row's off-diagonal magnitudes (diagonally dominant).
+static inline unsigned long long mix64(unsigned long long x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdULL;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ULL;
+  x ^= x >> 33;
+  return x;
+}
+
+static void flan_proxy_rows(int nx, int ny, int nz, long long first, int n_local, std::vector<long long> &rowptr,
+                            std::vector<long long> &gcols, std::vector<double> &vals) {
+  MIG_CHECK(nx % 2 == 1 && nx > 1 && ny > 0 && nz > 0, "FlanProxy: nx must be odd (coprime to 32)");
+  int ainv = 1;  // 32^-1 mod nx
+  while ((32LL * ainv) % nx != 1) ++ainv;
+  auto perm = [&](long long ix) { return (32 * ix + 7) % nx; };
+  auto unperm = [&](long long px) { return ((px - 7) % nx + nx) % nx * ainv % nx; };
+  const long long nxy = (long long)nx * ny;
+  rowptr.assign((size_t)n_local + 1, 0);
+  gcols.clear();
+  vals.clear();
+  gcols.reserve((size_t)n_local * 78);
+  vals.reserve((size_t)n_local * 78);
+  for (int r = 0; r < n_local; ++r) {
+    const long long g = first + r;
+    const long long pv = g / 3;
+    const long long iz = pv / nxy, iy = (pv % nxy) / nx, ix = unperm(pv % nx);
+    const long long v = ix + nx * (iy + ny * iz);
+    const size_t row0 = gcols.size();
+    size_t diag_at = 0;
+    double off = 0.0;
+    for (int dz = -1; dz <= 1; ++dz)
+      for (int dy = -1; dy <= 1; ++dy)
+        for (int dx = -1; dx <= 1; ++dx) {
+          const long long jx = ix + dx, jy = iy + dy, jz = iz + dz;
+          if (jx < 0 || jx >= nx || jy < 0 || jy >= ny || jz < 0 || jz >= nz) continue;
+          const long long u = jx + nx * (jy + ny * jz);
+          if (u != v && mix64((unsigned long long)std::min(u, v) * 0x9e3779b97f4a7c15ULL +
+                              (unsigned long long)std::max(u, v)) % 13 == 0)
+            continue;
+          const long long pu = perm(jx) + nx * (jy + ny * jz);
+          for (int e = 0; e < 3; ++e) {
+            const long long c = 3 * pu + e;
+            if (c == g) {
+              diag_at = gcols.size();
+              gcols.push_back(c);
+              vals.push_back(0.0);
+              continue;
+            }
+            const double h = (double)(mix64((unsigned long long)g * 0x100000001b3ULL ^ (unsigned long long)c) % 997);
+            const double a = -(h + 1.0) / 997.0;
+            gcols.push_back(c);
+            vals.push_back(a);
+            off += -a;
+          }
+        }
+    (void)row0;
+    vals[diag_at] = 1.0 + off;
+    rowptr[(size_t)r + 1] = (long long)gcols.size();
+  }
+}
+
 void galeri_rows(const std::string &kind, int nx, int ny, int nz, long long first, int n_local,
                  std::vector<long long> &rowptr, std::vector<long long> &gcols,
                  std::vector<double> &vals) {
+  if (kind == "FlanProxy") {
+    flan_proxy_rows(nx, ny, nz, first, n_local, rowptr, gcols, vals);
+    return;
+  }
   if (kind == "Brick3D") {
     const long long nxy = (long long)nx * ny;
     rowptr.assign((size_t)n_local + 1, 0);

@@ -982,7 +982,7 @@ extern "C" int migmres_crs_create_galeri(migmres_ctx *ctx, const char *kind, int
                                          migmres_crs **out) {
   return guard([&] {
     const std::string k(kind ? kind : "");
-    const long long n_global = (long long)nx * ny * (k == "Laplace3D" || k == "Brick3D" ? nz : 1);
+    const long long n_global = (long long)nx * ny * (k == "Laplace3D" || k == "Brick3D" ? nz : k == "FlanProxy" ? 3LL * nz : 1);
     long long first = 0;
     int n_local = 0;
     uniform_map(n_global, ctx->nranks, ctx->rank, &first, &n_local);

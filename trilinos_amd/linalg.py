@@ -96,6 +96,19 @@ def matrix_file_rows(path, first=0, n_local=None):
     return ng.value, rp, gc[:nnz.value], vv[:nnz.value]
 
 
+def galeri_rows(kind, nx, ny, nz, first, n_local):
+    """Host-only generator rows [first, first + n_local) (migmres_plan_galeri): rowptr, GLOBAL
+    columns in insertion order, values -- the rows CrsMatrix.galeri builds on each rank."""
+    nnz = C.c_longlong()
+    call("migmres_plan_galeri", kind.encode(), nx, ny, nz, first, n_local, None, None, None, C.byref(nnz))
+    rp = np.empty(n_local + 1, dtype=np.int64)
+    gc = np.empty(max(nnz.value, 1), dtype=np.int64)
+    vv = np.empty(max(nnz.value, 1), dtype=np.float64)
+    call("migmres_plan_galeri", kind.encode(), nx, ny, nz, first, n_local, lptr(rp), lptr(gc), dptr(vv),
+         C.byref(nnz))
+    return rp, gc[:nnz.value], vv[:nnz.value]
+
+
 class CrsMatrix:
     """Row-distributed CSR operator.  `rowptr`/`gcols`/`vals` are this rank's rows
     (uniform map) with GLOBAL column ids in insertion order; the library builds the
@@ -125,11 +138,12 @@ class CrsMatrix:
 
     @classmethod
     def galeri(cls, comm, kind, nx, ny, nz=1):
-        """Galeri::CreateCrsMatrix("Laplace2D"/"Laplace3D") on the uniform "Linear" map,
-        generated natively on each rank."""
+        """Galeri::CreateCrsMatrix("Laplace2D"/"Laplace3D"/"Brick3D") on the uniform "Linear"
+        map, generated natively on each rank; "FlanProxy" is the synthetic stand-in of config
+        4's Flan_1565 (3 nx ny nz rows, include/migmres.h)."""
         h = C.c_void_p()
         call("migmres_crs_create_galeri", comm.h, kind.encode(), nx, ny, nz, C.byref(h))
-        n = nx * ny * (nz if kind in ("Laplace3D", "Brick3D") else 1)
+        n = nx * ny * (nz if kind in ("Laplace3D", "Brick3D") else 3 * nz if kind == "FlanProxy" else 1)
         return cls(comm, n, _handle=h)
 
     @classmethod
