@@ -188,7 +188,9 @@ int migmres_mv_init(migmres_mv *mv, double alpha);                           /* 
  * *seed over the GLOBAL rows (partition independent); *seed is advanced. */
 int migmres_mv_random(migmres_mv *mv, unsigned int *seed);
 int migmres_mv_assign(const migmres_mv *A, migmres_mv *mv);                  /* Assign */
-int migmres_mv_set_block(const migmres_mv *A, const int *idx, int n, migmres_mv *mv); /* SetBlock */
+/* SetBlock: mv[:, idx[i]] = A[:, i] for i < n; A may have more than n columns (the first n are
+ * copied), as BelosEpetraAdapter.hpp:894-940. */
+int migmres_mv_set_block(const migmres_mv *A, const int *idx, int n, migmres_mv *mv);
 
 /* ---------------- ICGS orthogonalisation (Belos::ICGSOrthoManager) ---------------- */
 

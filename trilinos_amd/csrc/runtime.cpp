@@ -1129,15 +1129,21 @@ extern "C" int migmres_mv_assign(const migmres_mv *A, migmres_mv *mv) {
 }
 extern "C" int migmres_mv_set_block(const migmres_mv *A, const int *idx, int n, migmres_mv *mv) {
   return guard([&] {
-    MIG_CHECK(n == A->ncols, "SetBlock: index count must equal A's columns");
+    // BelosEpetraAdapter.hpp:894-940: A may have more columns than indices (its first n are
+    // copied), not fewer.
+    MIG_CHECK(n <= A->ncols, "SetBlock: A has fewer columns than there are indices");
     migmres_mv *v = mv_view(mv, idx, n);
+    migmres_mv *a = nullptr;
     try {
-      mv_assign(*A, *v);
+      a = n == A->ncols ? nullptr : mv_view_range(const_cast<migmres_mv *>(A), 0, n);
+      mv_assign(a ? *a : *A, *v);
       MIG_HIP(hipStreamSynchronize(mv->ctx->stream));
     } catch (...) {
+      delete a;
       delete v;
       throw;
     }
+    delete a;
     delete v;
   });
 }
