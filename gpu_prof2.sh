@@ -1,0 +1,5 @@
+source ./tools_gpu_check.sh
+export TMPDIR=/tmp
+P=${PROF:-k16b}
+step 300 rocprof_k16_$P.log rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof_k16_$P -o run -- python3 bench.py --no-cpu-baseline --k 16 --steps 25 --warmup 25 --no-profile
+step 300 rocprof_brick_$P.log rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof_brick_$P -o run -- python3 bench.py --no-cpu-baseline --matrix Brick3D --steps 25 --warmup 25 --no-profile

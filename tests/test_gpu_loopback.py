@@ -95,9 +95,16 @@ def test_distributed_spmm_bit_exact(kind, dims, k, P):
     assert np.array_equal(Y, Yref)
 
 
+@pytest.mark.parametrize("env", [{}, {"MIGMRES_FB_GRAM_GATE": "2"}, {"MIGMRES_FB_GRAM": "0"}])
 @pytest.mark.parametrize("kind,dims,k,nb,P", [("Laplace2D", (30, 30, 1), 2, 15, 2),
                                               ("Laplace3D", (12, 12, 12), 8, 5, 3)])
-def test_distributed_solve_matches_oracle(kind, dims, k, nb, P):
+def test_distributed_solve_matches_oracle(kind, dims, k, nb, P, env, monkeypatch):
+    """Distributed solves = the oracle, with findBasis in Gram form (default), with every
+    Gram block handed back to the column passes by the gate (per-rank sums, all-reduce, the
+    k x k step, the speculative SpMM with its halo exchange dropped, then the column passes:
+    ADVICE r1), and with the column passes only."""
+    for key, v in env.items():
+        monkeypatch.setenv(key, v)
     import trilinos_amd as ta
     from oracle import belos as ob, epetra as oe
     from tests.test_gpu_solver import _hist_close, oracle_rerun
@@ -129,6 +136,12 @@ def test_distributed_solve_matches_oracle(kind, dims, k, nb, P):
         assert iters == ref["iterations"]
         assert c["restarts"] == ref["restarts"] and c["applies"] == ref["n_apply"]
         assert c["explicit_checks"] == ref["n_explicit"]
+        if env.get("MIGMRES_FB_GRAM") == "0":
+            assert c["gram_calls"] == 0
+        elif env:
+            assert c["gram_skips"] == c["gram_calls"] > 0
+        else:
+            assert c["gram_calls"] > 0 and c["gram_skips"] == 0
         _hist_close(h, ref["history"], rerun)
     X = np.zeros((n, k))
     for r in res:

@@ -298,29 +298,43 @@ def test_dgks_orsirr1_reference_run(comm):
                 oracle_rerun(ob.solve, Aor.apply, b[:, None], dict(params, Orthogonalization="DGKS")))
 
 
+GRAM_KEYS = ("gram_calls", "gram_skips")
+
+
+@pytest.mark.parametrize("k", [4, 12, 16])
 @pytest.mark.parametrize("env", [{"MIGMRES_FB_GRAM": "0"}, {"MIGMRES_FB_GRAM_GATE": "2"},
                                  {"MIGMRES_FB_GRAM_FUSE": "0"}])
-def test_gram_findbasis_against_column_passes(comm, monkeypatch, env):
+def test_gram_findbasis_against_column_passes(comm, monkeypatch, env, k):
     """findBasis in Gram form (CholQR2 of the block with the reference's dependency tests on
-    its pivots; the default for ICGS with 2 <= k <= 8) against the column-by-column passes
+    its pivots; the default for ICGS with 2 <= k <= 16: k <= 8 with G1 taken by the closing
+    update, k > 8 by the MFMA Gram kernels) against the column-by-column passes
     (MIGMRES_FB_GRAM=0), against its own gate hand-back (gate 2: every block goes to the
     column passes, after the speculative SpMM has read it) and against its unfused form: the
-    same solver decisions and iteration counts, histories within the oracle bar."""
-    params = {"Block Size": 4, "Num Blocks": 10, "Maximum Iterations": 400, "Maximum Restarts": 40,
+    same solver decisions and iteration counts, histories within the oracle bar.  The Gram
+    counters show which path ran (a gram_ok regression must not pass silently)."""
+    params = {"Block Size": k, "Num Blocks": 10, "Maximum Iterations": 400, "Maximum Restarts": 40,
               "Convergence Tolerance": 1e-9, "Orthogonalization": "ICGS"}
-    sm, ret, X, _, _ = _device_solve(comm, "Laplace3D", (14, 13, 12), 4, 7, params)
+    sm, ret, X, _, _ = _device_solve(comm, "Laplace3D", (14, 13, 12), k, 7, params)
+    c = sm.counters()
+    assert c["gram_calls"] > 0 and c["gram_skips"] == 0, c
     for key, v in env.items():
         monkeypatch.setenv(key, v)
-    sm2, ret2, X2, _, _ = _device_solve(comm, "Laplace3D", (14, 13, 12), 4, 7, params)
-    c = sm.counters()
+    sm2, ret2, X2, _, _ = _device_solve(comm, "Laplace3D", (14, 13, 12), k, 7, params)
+    c2 = sm2.counters()
     assert ret2 == ret and sm2.getNumIters() == sm.getNumIters()
-    assert sm2.counters() == c
+    assert {a: b for a, b in c2.items() if a not in GRAM_KEYS} == {a: b for a, b in c.items() if a not in GRAM_KEYS}
+    if env.get("MIGMRES_FB_GRAM") == "0":
+        assert c2["gram_calls"] == 0
+    elif "MIGMRES_FB_GRAM_GATE" in env:
+        assert c2["gram_skips"] == c2["gram_calls"] == c["gram_calls"]
+    else:
+        assert c2["gram_calls"] == c["gram_calls"] and c2["gram_skips"] == 0
 
     def drift():
         from oracle import belos as ob, epetra as oe
         n, gen = _gen("Laplace3D", (14, 13, 12))
         Aor = oe.DistCrs(gen, n, 1)
-        Xex, _ = oe.epetra_random_mv(7, n, 4)
+        Xex, _ = oe.epetra_random_mv(7, n, k)
         B = Aor.apply(Xex)
         h1 = ob.solve(Aor.apply, B, params)["history"]
         # the first GPU history shifted by the oracle's summation-order drift

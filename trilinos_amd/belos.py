@@ -326,10 +326,10 @@ class BlockGmresSolMgr:
         return out[:nr.value * nc.value].reshape(nr.value, nc.value)
 
     def counters(self):
-        out = (C.c_longlong * 7)()
-        call("migmres_solver_counters", self.h, out, 7)
+        out = (C.c_longlong * 9)()
+        call("migmres_solver_counters", self.h, out, 9)
         keys = ("applies", "explicit_checks", "restarts", "blk_ortho_sing", "block_iterations",
-                "prec_applies", "deflations")
+                "prec_applies", "deflations", "gram_calls", "gram_skips")
         return dict(zip(keys, list(out)))
 
     def timers(self):

@@ -19,9 +19,11 @@ struct IcgsState {
   int gram_pad_;
 };
 
-// findBasis in Gram form (icgs.hip; ICGS with two passes, 2 <= k <= 8).  The partial-writing
-// launchers return their number of workgroups (rows of partials, at most 1024), stored
-// value-major (partial[i * nb + b]): the packed upper triangle of the k x k Gram matrix.
+// findBasis in Gram form (icgs.hip; ICGS with two passes, 2 <= k <= 16).  The partial-writing
+// launchers return their number of workgroups (rows of partials, at most 1024): the packed
+// upper triangle of the k x k Gram matrix, value-major (partial[i * nb + b]) for k <= 8 (read
+// by launch_fbg_chol), block-major (partial[b * nv + i]) for k > 8 (launch_reduce_partials,
+// then launch_fbg_chol_l).  launch_gemm_nn_gram: k <= 8 only.
 // w: 768 doubles of device scratch (T1, T2, R1).
 int launch_gemm_nn_gram(hipStream_t s, MvDesc A, int L, const double *M, int ldm, MvDesc X, int nrows,
                         double *partial);
@@ -32,6 +34,8 @@ void launch_fbg_b(hipStream_t s, MvDesc X, int k, int nrows, const IcgsState *st
 // stage 0: sums of the partials only (-> sums); 1: dependency test, R1, gate, T1; 2: R2, T2, B
 void launch_fbg_chol(hipStream_t s, const double *partial, int nblocks, int k, int stage, IcgsState *st, double *w,
                      double gate, double *sums);
+// the same step for k > 8 from the summed Gram matrix (nv = k(k+1)/2 values)
+void launch_fbg_chol_l(hipStream_t s, const double *gsum, int k, int stage, IcgsState *st, double *w, double gate);
 
 // Pass prologue: the reduction + scalar step still pending from the previous pass, taken by
 // every workgroup of the next pass from the previous pass's per-workgroup partials (one

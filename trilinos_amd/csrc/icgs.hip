@@ -19,6 +19,7 @@
 namespace migmres {
 
 typedef double d2 __attribute__((ext_vector_type(2)));
+typedef double d4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ double *colp_(const MvDesc &d, int c) {
   return d.base + (long long)(d.cols ? d.cols[c] : c) * d.ld;
@@ -595,10 +596,26 @@ static size_t nw_lds_bytes(int L, int NJ) {
 
 template <int RW, int NM, int NJ, bool ST>
 __global__ __launch_bounds__(16 * RW) void k_nn_tn_w(MvDesc Q, int L, const double *__restrict__ C1, int ldc,
-                                                     MvDesc X, int k, int nrows, double *__restrict__ partial,
+                                                     MvDesc X, int kx, int nrows, double *__restrict__ partial,
                                                      double *__restrict__ sink) {
   constexpr int NTH = 16 * RW, NWAVE = NTH / 64, RB = RW / 16, LDQ = RW + 1, LPC = RW / 2;
   extern __shared__ __attribute__((aligned(16))) double sm[];
+  // kx > 8: workgroup pairs take the two column halves of X (columns h0 .. h0 + k - 1) over
+  // the same chunk range at the same time and on the same XCD (blocks 16 q + x and
+  // 16 q + x + 8, x < 8; block b is dispatched to XCD b mod 8), so each chunk of Q comes from
+  // HBM once and the pair's second read hits that XCD's L2 or the Infinity Cache.  Partials:
+  // half 0 at [rng][L][8], half 1 after all nrng of them at [rng][L][kx - 8].
+  int rng = blockIdx.x, nrng = gridDim.x, h0 = 0;
+  if (kx > 8) {
+    const int x = blockIdx.x & 15;
+    h0 = (x >> 3) * 8;
+    rng = (blockIdx.x >> 4) * 8 + (x & 7);
+    nrng = gridDim.x >> 1;
+  }
+  const int k = kx > 8 ? (h0 ? kx - 8 : 8) : kx;
+  C1 += (long long)h0 * ldc;
+  double *const pout = partial + (long long)(h0 ? nrng : 0) * L * 8 + (long long)rng * L * k;
+  auto xcol = [&](int j) { return colp_(X, h0 + j); };
   const int LX = L + k;
   const int Lp = (L + 4 * NJ + 15) & ~15, Lq = (L + 15) & ~15;
   double *Qs = sm;
@@ -611,9 +628,11 @@ __global__ __launch_bounds__(16 * RW) void k_nn_tn_w(MvDesc Q, int L, const doub
     const int i = e / (4 * NJ), j = e % (4 * NJ);
     C1s[e] = (i < L && j < k) ? C1[i + (long long)j * ldc] : 0.0;
   }
-  double acc2[(16 + NWAVE - 1) / NWAVE][NJ];
+  // 16-column tiles of the staged image: 2 NM (L + k <= 32 NM), shared round-robin by the waves
+  constexpr int NTILE = 2 * NM, TPW = (NTILE + NWAVE - 1) / NWAVE;
+  double acc2[TPW][NJ];
 #pragma unroll
-  for (int m = 0; m < (16 + NWAVE - 1) / NWAVE; ++m)
+  for (int m = 0; m < TPW; ++m)
 #pragma unroll
     for (int jg = 0; jg < NJ; ++jg) acc2[m][jg] = 0.0;
 
@@ -627,33 +646,35 @@ __global__ __launch_bounds__(16 * RW) void k_nn_tn_w(MvDesc Q, int L, const doub
     int i = lcol + 32 * m;
     i = i < LX ? i : LX - 1;
     lsts[m] = i * LDQ + lrow;
-    lsrc[m] = (i < L ? Q.base + (long long)i * Q.ld : colp_(X, i - L)) + lrow;
+    lsrc[m] = (i < L ? Q.base + (long long)i * Q.ld : xcol(i - L)) + lrow;
   }
   // X1 element e = t mod (RW k): row xr of column xj.  Threads t >= RW k repeat an element
   // and store the same value again, so the X1 store is unconditional: a conditional store
   // makes the compiler drain the whole prefetch (vmcnt(0)) at the top of the next chunk.
   const int xe = t % (RW * k), xr = xe % RW, xj = xe / RW;
   const bool xprim = t < RW * k;
-  double *xdst = colp_(X, xj);
+  double *xdst = xcol(xj);
   const int xjg = xj >> 2;
   const int xr16 = xr & 15, xrb = xr >> 4;
   const int xo = 16 * (xr16 & 3) + 4 * (xr16 >> 2) + (xj & 3);  // D lane of (row, column)
   double *xs = Qs + (size_t)(L + xj) * LDQ + xr;
   const long long nchunks = (nrows + RW - 1) / RW;
-  const long long c0 = nchunks * blockIdx.x / gridDim.x, c1 = nchunks * (blockIdx.x + 1) / gridDim.x;
-  auto clampc = [&](long long chunk) { return chunk < c1 ? chunk : c1 - 1; };
+  const long long c0 = nchunks * rng / nrng, c1 = nchunks * (rng + 1) / nrng;
 
   // 1-deep register prefetch: the next chunk's loads are issued right after the barrier
   // that publishes the current one and stay in flight through both phases.  Rows past nrows
-  // are zero padding in Q and X, so their X1 is zero and is stored back unguarded.
+  // are zero padding in Q and X, so their X1 is zero and is stored back unguarded.  (A
+  // 2-deep prefetch at one workgroup per CU measured no faster: at large L the kernel is
+  // bound by its LDS reads -- about 200 ds_read_b64 per wave per chunk -- not by latency.)
+  auto clampc = [&](long long chunk) { return chunk < c1 ? chunk : c1 - 1; };
   d2 p[NM];
 #pragma unroll
-  for (int m = 0; m < NM; ++m) p[m] = *(const d2 *)(lsrc[m] + c0 * RW);
+  for (int m = 0; m < NM; ++m) p[m] = *(const d2 *)(lsrc[m] + (c0 < c1 ? c0 : nchunks - 1) * RW);  // empty range (k > 8, few chunks): any valid chunk
   // A store behind the prologue loads, like the X1 store behind the in-loop prefetch: the
   // loop header then sees the same pending-event order on both incoming edges and waits
   // vmcnt(1) for the last prefetched column instead of vmcnt(0) (which waits for the X1
   // store's completion).  partial[0] of this workgroup is rewritten at the end.
-  if ((NT_DIAG_MASK & 8) && ST) partial[(long long)blockIdx.x * L * k] = 0.0;
+  if ((NT_DIAG_MASK & 8) && ST) pout[0] = 0.0;
   for (long long ch = c0; ch < c1; ++ch) {
     {
       const long long r0 = ch * RW;
@@ -673,12 +694,12 @@ __global__ __launch_bounds__(16 * RW) void k_nn_tn_w(MvDesc Q, int L, const doub
         for (int m = 0; m < NM; ++m) p[m] = *(const d2 *)(lsrc[m] + cn);
       }
       const double xval = *xs;
-      // phase 1: rows 16 rb .. 16 rb + 15, K steps s = kq + 4 m
+      // phase 1: rows 16 rb .. 16 rb + 15, K steps s = kq + 4 m (4 s < L <= 32 NM)
       double a1[NJ];
 #pragma unroll
       for (int jg = 0; jg < NJ; ++jg) a1[jg] = 0.0;
 #pragma unroll
-      for (int m = 0; m < ((NT_DIAG_MASK & 1) ? 16 : 0); ++m) {
+      for (int m = 0; m < ((NT_DIAG_MASK & 1) ? 2 * NM : 0); ++m) {
         const int s = kq + 4 * m;
         if (4 * s < L) {
           const double qa = Qs[(4 * s + g) * LDQ + 16 * rb + c];
@@ -699,7 +720,7 @@ __global__ __launch_bounds__(16 * RW) void k_nn_tn_w(MvDesc Q, int L, const doub
       lds_barrier();
       // phase 2: tiles w, w + NWAVE, ... against the RW rows of X1 (staged columns L + j)
 #pragma unroll
-      for (int mm = 0; mm < ((NT_DIAG_MASK & 2) ? (16 + NWAVE - 1) / NWAVE : 0); ++mm) {
+      for (int mm = 0; mm < ((NT_DIAG_MASK & 2) ? TPW : 0); ++mm) {
         const int tt = w + NWAVE * mm;
         if (16 * tt < L) {
 #pragma unroll
@@ -715,9 +736,9 @@ __global__ __launch_bounds__(16 * RW) void k_nn_tn_w(MvDesc Q, int L, const doub
     }
   }
   // partial (L x k) of this workgroup: tile tt rows 16 tt + 4 b + m
-  double *out = partial + (long long)blockIdx.x * L * k;
+  double *out = pout;
 #pragma unroll
-  for (int mm = 0; mm < (16 + NWAVE - 1) / NWAVE; ++mm) {
+  for (int mm = 0; mm < TPW; ++mm) {
     const int tt = w + NWAVE * mm;
     const int i = 16 * tt + 4 * ((l >> 2) & 3) + (l >> 4);
 #pragma unroll
@@ -766,22 +787,28 @@ constexpr int NW_WG_PER_CU = NT_WIDE_WGCU;
 template <int RW, int NJ, bool ST>
 static nt_kernel_t nw_pick_nm(int LX) {
   switch ((LX + 31) >> 5) {
-    case 1: return k_nn_tn_w<RW, 1, NJ, ST>;
-    case 2: return k_nn_tn_w<RW, 2, NJ, ST>;
-    case 3: return k_nn_tn_w<RW, 3, NJ, ST>;
-    case 4: return k_nn_tn_w<RW, 4, NJ, ST>;
-    case 5: return k_nn_tn_w<RW, 5, NJ, ST>;
-    case 6: return k_nn_tn_w<RW, 6, NJ, ST>;
-    case 7: return k_nn_tn_w<RW, 7, NJ, ST>;
-    default: return k_nn_tn_w<RW, 8, NJ, ST>;
+#define NW_CASE(N) \
+  case N:          \
+    return k_nn_tn_w<RW, N, NJ, ST>;
+    NW_CASE(1) NW_CASE(2) NW_CASE(3) NW_CASE(4) NW_CASE(5) NW_CASE(6) NW_CASE(7) NW_CASE(8)
+    NW_CASE(9) NW_CASE(10) NW_CASE(11) NW_CASE(12) NW_CASE(13) NW_CASE(14) NW_CASE(15)
+#undef NW_CASE
+    default: return k_nn_tn_w<RW, 16, NJ, ST>;
   }
 }
 
 
 // The wide variant wins from L = 64 on (256^3, k = 8); below that the per-chunk latency
-// is not hidden.  It needs NW_WG_PER_CU workgroups' LDS to fit in 160 KiB.
+// is not hidden.  Up to L + k = 256 NW_WG_PER_CU workgroups' LDS fit in 160 KiB; wider
+// images (k = 16 in column halves: L up to 400 at Num Blocks 25) run one workgroup per CU.
+static int nw_wg_per_cu(int L, int k) {
+  const size_t lds = nw_lds_bytes<NW_RW>(L, (k + 3) >> 2);
+  const int fit = (int)((160 * 1024) / lds);
+  return fit < NW_WG_PER_CU ? fit : NW_WG_PER_CU;
+}
 static bool nw_ok(int L, int k) {
-  return L >= 64 && k <= 8 && L + k <= 256 && nw_lds_bytes<NW_RW>(L, (k + 3) >> 2) * NW_WG_PER_CU <= 160 * 1024;
+  if (k > 8) return k <= 16 && nw_ok(L, 8);  // column halves in one launch
+  return L >= 64 && L + k <= 512 && nw_wg_per_cu(L, k) >= 1;
 }
 
 static int cu_count() {
@@ -797,8 +824,15 @@ static int cu_count() {
 
 int nn_tn_blocks(int nrows, int L, int k) {
   if (nw_ok(L, k)) {
+    const int kh = k > 8 ? 8 : k;
     const long long nchunks = (nrows + NW_RW - 1) / NW_RW;
-    const long long want = (long long)NW_WG_PER_CU * cu_count();
+    const long long want = (long long)nw_wg_per_cu(L, kh) * cu_count();
+    if (k > 8) {  // pairs of workgroups per chunk range, ranges in groups of 8 (one per XCD)
+      long long r = (want / 2) / 8 * 8;
+      if (r > nchunks) r = nchunks / 8 * 8;
+      if (r < 8) r = 8;
+      return (int)(2 * r);
+    }
     const long long b = want < nchunks ? want : nchunks;
     return b < 1 ? 1 : (int)b;
   }
@@ -812,20 +846,24 @@ int nn_tn_blocks(int nrows, int L, int k) {
   return b < 1 ? 1 : (int)b;
 }
 
-bool nn_tn_supported(int L, int k) { return L >= 1 && L <= NT_MAXL && k >= 1 && k <= 16; }
+bool nn_tn_supported(int L, int k) { return L >= 1 && k >= 1 && k <= 16 && (L <= NT_MAXL || nw_ok(L, k)); }
 
 void launch_nn_tn(hipStream_t s, MvDesc Q, int L, const double *C1, int ldc, MvDesc X, int nrows,
                   double *partial, int nblocks, double *sink, bool store_x1) {
   const int k = X.ncols;
-  if (!nn_tn_supported(L, k)) throw Error(MIGMRES_EINVAL, "nn_tn: 1 <= L <= 256 and 1 <= k <= 16");
+  if (!nn_tn_supported(L, k))
+    throw Error(MIGMRES_EINVAL, "nn_tn: 1 <= k <= 16 and L <= 256 (L + k <= 512 for k <= 8, L >= 64)");
   if (Q.cols) throw Error(MIGMRES_EINVAL, "nn_tn: Q must be a contiguous column range");
   if (nw_ok(L, k)) {
-    const int NJ = (k + 3) >> 2;
-    nt_kernel_t f = store_x1 ? (NJ == 1 ? nw_pick_nm<NW_RW, 1, true>(L + k) : nw_pick_nm<NW_RW, 2, true>(L + k))
-                             : (NJ == 1 ? nw_pick_nm<NW_RW, 1, false>(L + k) : nw_pick_nm<NW_RW, 2, false>(L + k));
+    if (k > 8 && (nblocks % 16 != 0 || (long long)(nblocks / 2) > ((long long)nrows + NW_RW - 1) / NW_RW + 7))
+      throw Error(MIGMRES_EINVAL, "nn_tn: k > 8 needs a grid of 16 q workgroups (nn_tn_blocks)");
+    const int NJ = k > 8 ? 2 : (k + 3) >> 2;
+    const int kh = k > 8 ? 8 : k;
+    nt_kernel_t f = store_x1 ? (NJ == 1 ? nw_pick_nm<NW_RW, 1, true>(L + kh) : nw_pick_nm<NW_RW, 2, true>(L + kh))
+                             : (NJ == 1 ? nw_pick_nm<NW_RW, 1, false>(L + kh) : nw_pick_nm<NW_RW, 2, false>(L + kh));
     const size_t lds = nw_lds_bytes<NW_RW>(L, NJ);
-    static bool attr_set[2][2][9] = {};
-    const int nm = (L + k + 31) >> 5;
+    static bool attr_set[2][2][17] = {};
+    const int nm = (L + kh + 31) >> 5;
     if (!attr_set[store_x1][NJ - 1][nm]) {
       if (hipFuncSetAttribute((const void *)f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
         throw Error(MIGMRES_EHIP, "nn_tn: cannot raise the dynamic LDS limit");
@@ -1566,6 +1604,196 @@ __global__ __launch_bounds__(FBG_NT) void k_fbg_b(MvDesc X, int nrows, const Icg
   }
 }
 
+// findBasis in Gram form for 9 <= k <= 16.  A row pair's k(k+1)/2 register sums and the
+// hoisted T matrices no longer fit (k_fbg_b<16> spilled 708 B per lane and ran at 1.9 TB/s),
+// so both products run on v_mfma_f64_16x16x4f64:
+//  * X T in the transposed form (X T)^T = T^T X^T, 16 rows per MFMA chain: the B operand of
+//    step s is X[r0 + (l & 15)][4 s + (l >> 4)] (16 rows of a column: one 128-B segment per
+//    16 lanes), the A operand T[4 s + (l >> 4)][l & 15] (4 registers per lane for the whole
+//    launch), and D[q] = (X T)[r0 + (l & 15)][4 q + (l >> 4)] -- exactly the B operand of step
+//    q of a second product, so (X T1) T2 needs no transpose;
+//  * the Gram matrix: each wave writes its 128 rows x 16 columns to LDS column-major (stride
+//    FBM_S) and accumulates G = Y^T Y, whose A and B operands are then the same element.
+// Y = X T1 is formed by the same MFMA sequence in k_fbg_gram_m<K, true> and k_fbg_b_m, so the
+// block k_fbg_b_m writes is (Y T2) of the Y whose Gram matrix gave T2.  Columns >= k are zero.
+constexpr int FBM_S = 132;  // 128 rows + 4 (LDS column stride)
+
+template <int K>
+__device__ __forceinline__ void fbm_coef(const double *__restrict__ w, double (&a)[4]) {
+  const int l = threadIdx.x & 63, c = l & 15;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int i = 4 * s + (l >> 4);
+    a[s] = (i <= c && c < K) ? w[i + 16 * c] : 0.0;
+  }
+}
+__device__ __forceinline__ d4 fbm_mul(const double (&a)[4], const double (&b)[4]) {
+  d4 d = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int s = 0; s < 4; ++s) d = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], b[s], d, 0, 0, 0);
+  return d;
+}
+// per-lane column pointers of the B-operand layout: column 4 s + (l >> 4), nullptr past k
+template <int K>
+__device__ __forceinline__ void fbm_cols(const MvDesc &X, double *(&xp)[4]) {
+  const int l = threadIdx.x & 63;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int c = 4 * s + (l >> 4);
+    xp[s] = c < K ? colp_(X, c) : nullptr;
+  }
+}
+
+// APPLY: partials of G2 = (X T1)^T (X T1) (k_fbg_a); else of G1 = X^T X (k_fbg_gram).
+// Partials block-major (partial[b * NV + i]) for launch_reduce_partials.
+template <int K, bool APPLY>
+__global__ __launch_bounds__(FBG_NT) void k_fbg_gram_m(MvDesc X, int nrows, const IcgsState *__restrict__ st,
+                                                      const double *__restrict__ w, double *__restrict__ partial,
+                                                      int rev) {
+  if (APPLY && st->gram_skip) return;
+  constexpr int NV = K * (K + 1) / 2, NW = FBG_NT / 64;
+  __shared__ __attribute__((aligned(16))) double tile[NW][16 * FBM_S];
+  __shared__ double red[NW][NV];
+  const int l = threadIdx.x & 63, wv = threadIdx.x >> 6, lr = l & 15, lc = l >> 4;
+  double *tw = tile[wv];
+  double a1[4] = {0.0, 0.0, 0.0, 0.0};
+  if (APPLY) fbm_coef<K>(w, a1);
+  double *xp[4];
+  fbm_cols<K>(X, xp);
+  d4 acc = {0.0, 0.0, 0.0, 0.0};
+  const long long nq = ((long long)nrows + 127) / 128;
+  for (long long q = (long long)blockIdx.x * NW + wv; q < nq; q += (long long)gridDim.x * NW) {
+    const long long r0 = 128 * (rev ? nq - 1 - q : q);
+    double xv[8][4];
+#pragma unroll
+    for (int g = 0; g < 8; ++g)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) xv[g][s] = xp[s] ? xp[s][r0 + 16 * g + lr] : 0.0;  // rows >= nrows: zero padding
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      if (APPLY) {
+        const d4 y = fbm_mul(a1, xv[g]);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) xv[g][s] = y[s];
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s) tw[(4 * s + lc) * FBM_S + 16 * g + lr] = xv[g][s];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own stores before its reads
+#pragma unroll
+    for (int s = 0; s < 32; ++s) {
+      const double a = tw[lr * FBM_S + 4 * s + lc];
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, a, acc, 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next stores
+  }
+  // lane l holds G[(l >> 4) + 4 q][l & 15], q = 0..3
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int i = lc + 4 * q, j = lr;
+    if (i <= j && j < K) red[wv][j * (j + 1) / 2 + i] = acc[q];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < NV; i += FBG_NT)
+    partial[(long long)blockIdx.x * NV + i] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
+}
+
+// X <- (X T1) T2 for 9 <= k <= 16 (k_fbg_b's step), both products on MFMA as above
+template <int K>
+__global__ __launch_bounds__(FBG_NT) void k_fbg_b_m(MvDesc X, int nrows, const IcgsState *__restrict__ st,
+                                                   const double *__restrict__ w, int rev) {
+  if (st->gram_skip) return;
+  constexpr int NW = FBG_NT / 64;
+  const int l = threadIdx.x & 63, wv = threadIdx.x >> 6, lr = l & 15;
+  double a1[4], a2[4];
+  fbm_coef<K>(w, a1);
+  fbm_coef<K>(w + 256, a2);
+  double *xp[4];
+  fbm_cols<K>(X, xp);
+  const long long nq = ((long long)nrows + 63) / 64;
+  for (long long q = (long long)blockIdx.x * NW + wv; q < nq; q += (long long)gridDim.x * NW) {
+    const long long r0 = 64 * (rev ? nq - 1 - q : q);
+    double xv[4][4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) xv[g][s] = xp[s] ? xp[s][r0 + 16 * g + lr] : 0.0;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const d4 y = fbm_mul(a1, xv[g]);
+      double yb[4] = {y[0], y[1], y[2], y[3]};
+      const d4 z = fbm_mul(a2, yb);
+      const long long r = r0 + 16 * g + lr;
+      if (r < nrows) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          if (xp[s]) xp[s][r] = z[s];
+      }
+    }
+  }
+}
+
+// The k x k step of k_fbg_chol for 9 <= k <= 16 on the summed Gram matrix (packed upper
+// triangle in g): the same operations in the same order per element, with R and T in LDS and
+// the independent elements on separate threads (one thread would hold 400+ live doubles).
+__global__ __launch_bounds__(256) void k_fbg_chol_l(const double *__restrict__ gsum, int k, int stage,
+                                                   IcgsState *st, double *__restrict__ w, double gate) {
+  __shared__ double g[136], R[16][17], T[16][17];
+  __shared__ int ok;
+  const int t = threadIdx.x, nv = k * (k + 1) / 2;
+  if (t < nv) g[t] = gsum[t];
+  if (t == 0) ok = 1;
+  __syncthreads();
+  if (stage == 2 && st->gram_skip) return;
+  if (stage == 1 && t == 0) {
+    st->gram_skip = 0;
+    bool dep = false;
+    for (int c = 0; c < k; ++c) dep = dep || fabs(g[c * (c + 1) / 2 + c]) < fabs(st->blk_old[c] * st->blk_tol);
+    if (dep) st->dep = 1.0;
+  }
+  for (int j = 0; j < k; ++j) {
+    if (t == 0) {
+      const double gjj = g[j * (j + 1) / 2 + j];
+      double s = gjj;
+      for (int i = 0; i < j; ++i) s -= R[i][j] * R[i][j];
+      if (!(gjj > 0.0 && s >= gate * gjj)) ok = 0;
+      R[j][j] = sqrt(fabs(s));
+    }
+    __syncthreads();
+    if (t > j && t < k) {
+      double v = g[t * (t + 1) / 2 + j];
+      for (int i = 0; i < j; ++i) v -= R[i][j] * R[i][t];
+      R[j][t] = v / R[j][j];
+    }
+    __syncthreads();
+  }
+  if (!ok) {
+    if (t == 0) st->gram_skip = 1;
+    return;
+  }
+  if (t < k) {  // column t of T = R^{-1}
+    const int c = t;
+    T[c][c] = 1.0 / R[c][c];
+    for (int i = c - 1; i >= 0; --i) {
+      double v = 0.0;
+      for (int m = i + 1; m <= c; ++m) v += R[i][m] * T[m][c];
+      T[i][c] = -v / R[i][i];
+    }
+    double *Tout = w + (stage == 1 ? 0 : 256);
+    for (int i = 0; i <= c; ++i) Tout[i + 16 * c] = T[i][c];
+    if (stage == 1)
+      for (int i = 0; i <= c; ++i) w[512 + i + 16 * c] = R[i][c];
+  }
+  if (stage == 2 && t < nv) {  // B = R2 R1, element (i, c) of the packed upper triangle
+    int c = 0;
+    while ((c + 1) * (c + 2) / 2 <= t) ++c;
+    const int i = t - c * (c + 1) / 2;
+    double v = 0.0;
+    for (int m = i; m <= c; ++m) v += R[i][m] * w[512 + m + 16 * c];
+    st->B[i + 16 * c] = v;
+  }
+}
+
 // One workgroup: the fixed-order sum of the partial rows, then thread 0 takes the step.
 // Templated on k so that G, R and T are register arrays (fully unrolled): the k x k
 // factorisations are a chain of dependent operations, which through LDS cost tens of us.
@@ -1692,6 +1920,7 @@ static int fbg_nb(int resident, int nrows) {
 }
 
 #define FBG_CASES(M) M(2) M(3) M(4) M(5) M(6) M(7) M(8)
+#define FBM_CASES(M) M(9) M(10) M(11) M(12) M(13) M(14) M(15) M(16)
 
 int launch_gemm_nn_gram(hipStream_t s, MvDesc A, int L, const double *M, int ldm, MvDesc X, int nrows,
                         double *partial) {
@@ -1715,7 +1944,7 @@ int launch_gemm_nn_gram(hipStream_t s, MvDesc A, int L, const double *M, int ldm
 }
 
 int launch_fbg_gram(hipStream_t s, MvDesc X, int k, int nrows, double *partial, int rev) {
-  static int occ[9];
+  static int occ[17];
   int nb = 1;
   switch (k) {
 #define FG_CASE(K)                                                 \
@@ -1726,8 +1955,16 @@ int launch_fbg_gram(hipStream_t s, MvDesc X, int k, int nrows, double *partial, 
     break;
     FBG_CASES(FG_CASE)
 #undef FG_CASE
+#define FGM_CASE(K)                                                                      \
+  case K:                                                                                \
+    if (!occ[K]) occ[K] = fbg_resident(k_fbg_gram_m<K, false>, 0);                       \
+    nb = fbg_nb(occ[K], nrows);                                                          \
+    k_fbg_gram_m<K, false><<<nb, FBG_NT, 0, s>>>(X, nrows, nullptr, nullptr, partial, rev); \
+    break;
+    FBM_CASES(FGM_CASE)
+#undef FGM_CASE
     default:
-      throw Error(MIGMRES_EINVAL, "fbg_gram: 2 <= k <= 8");
+      throw Error(MIGMRES_EINVAL, "fbg_gram: 2 <= k <= 16");
   }
   LAUNCH_CHECK_();
   return nb;
@@ -1735,7 +1972,7 @@ int launch_fbg_gram(hipStream_t s, MvDesc X, int k, int nrows, double *partial, 
 
 int launch_fbg_a(hipStream_t s, MvDesc X, int k, int nrows, const IcgsState *st, const double *w, double *partial,
                  int rev) {
-  static int occ[9];
+  static int occ[17];
   int nb = 1;
   switch (k) {
 #define FA_CASE(K)                                                       \
@@ -1746,15 +1983,23 @@ int launch_fbg_a(hipStream_t s, MvDesc X, int k, int nrows, const IcgsState *st,
     break;
     FBG_CASES(FA_CASE)
 #undef FA_CASE
+#define FAM_CASE(K)                                                                 \
+  case K:                                                                           \
+    if (!occ[K]) occ[K] = fbg_resident(k_fbg_gram_m<K, true>, 0);                   \
+    nb = fbg_nb(occ[K], nrows);                                                     \
+    k_fbg_gram_m<K, true><<<nb, FBG_NT, 0, s>>>(X, nrows, st, w, partial, rev);     \
+    break;
+    FBM_CASES(FAM_CASE)
+#undef FAM_CASE
     default:
-      throw Error(MIGMRES_EINVAL, "fbg_a: 2 <= k <= 8");
+      throw Error(MIGMRES_EINVAL, "fbg_a: 2 <= k <= 16");
   }
   LAUNCH_CHECK_();
   return nb;
 }
 
 void launch_fbg_b(hipStream_t s, MvDesc X, int k, int nrows, const IcgsState *st, const double *w, int rev) {
-  static int occ[9];
+  static int occ[17];
   switch (k) {
 #define FB2_CASE(K)                                                               \
   case K:                                                                         \
@@ -1763,8 +2008,15 @@ void launch_fbg_b(hipStream_t s, MvDesc X, int k, int nrows, const IcgsState *st
     break;
     FBG_CASES(FB2_CASE)
 #undef FB2_CASE
+#define FBM2_CASE(K)                                                                  \
+  case K:                                                                             \
+    if (!occ[K]) occ[K] = fbg_resident(k_fbg_b_m<K>, 0);                              \
+    k_fbg_b_m<K><<<fbg_nb(occ[K], nrows), FBG_NT, 0, s>>>(X, nrows, st, w, rev);      \
+    break;
+    FBM_CASES(FBM2_CASE)
+#undef FBM2_CASE
     default:
-      throw Error(MIGMRES_EINVAL, "fbg_b: 2 <= k <= 8");
+      throw Error(MIGMRES_EINVAL, "fbg_b: 2 <= k <= 16");
   }
   LAUNCH_CHECK_();
 }
@@ -1781,6 +2033,12 @@ void launch_fbg_chol(hipStream_t s, const double *partial, int nblocks, int k, i
     default:
       throw Error(MIGMRES_EINVAL, "fbg_chol: 2 <= k <= 8");
   }
+  LAUNCH_CHECK_();
+}
+
+void launch_fbg_chol_l(hipStream_t s, const double *gsum, int k, int stage, IcgsState *st, double *w, double gate) {
+  if (k < 2 || k > 16) throw Error(MIGMRES_EINVAL, "fbg_chol_l: 2 <= k <= 16");
+  k_fbg_chol_l<<<1, 256, 0, s>>>(gsum, k, stage, st, w, gate);
   LAUNCH_CHECK_();
 }
 

@@ -305,7 +305,7 @@ struct FastIcgs {
   bool use_fused = true;  // MIGMRES_NO_FUSED_NN_TN=1 selects the two-kernel form (A/B timing)
   int fb_rev = 1;         // findBasis b2 passes sweep rows top-down (MIGMRES_FB_REV=0: all bottom-up)
   bool x1_store = false;  // fused pass writes X1 back (MIGMRES_NN_TN_STORE=1, A/B timing)
-  int nt_cache[257][4] = {};
+  int nt_cache[1025][4] = {};
   // findBasis in Gram form (icgs.hip k_fbg_*; ICGS with two passes, 2 <= k <= 8).
   // MIGMRES_FB_GRAM=0 keeps the column passes; MIGMRES_FB_GRAM_FUSE=0 takes G1 in a pass of
   // its own instead of in the closing update; MIGMRES_FB_GRAM_GATE overrides the pivot-ratio
@@ -370,7 +370,8 @@ struct FastIcgs {
     const char *xs = std::getenv("MIGMRES_NN_TN_STORE");
     x1_store = xs && xs[0] == '1';
     const size_t np = std::max({(size_t)nblk_tn * 512 * 16, (size_t)nblk_ic * 17,
-                                (size_t)nn_tn_blocks(nl, 16, 1) * 256 * 16});
+                                (size_t)nn_tn_blocks(nl, 16, 1) * 256 * 16,
+                                (size_t)1024 * (size_t)std::min(lmax, 1024) * 8});  // wide nn_tn halves
     MIG_HIP(hipMalloc(&partial, sizeof(double) * np));
     MIG_HIP(hipMalloc(&R1, sizeof(double) * (size_t)(lmax + k) * k));
     MIG_HIP(hipMalloc(&R2, sizeof(double) * (size_t)(lmax + k) * k));
@@ -488,6 +489,23 @@ struct FastIcgs {
     // Measured at 256^3, k = 8 (tools/mb_lib.cpp): the fused kernel beats the two streaming
     // kernels from L = 16 on (1.3 vs 1.4 ms at L = 16, 9.0 vs 10.5 ms at L = 200).
     const bool fused_wins = L >= 16;
+    // k > 8 (L >= 64): both 8-column halves of X in one launch of the wide fused kernel, the
+    // two workgroups of a chunk range on one XCD (Q from HBM once; each column of X1 and of
+    // C2 depends on its own column of X and C1 only, so the halves are the same arithmetic);
+    // the narrow kernel ran at 1.65 TB/s at k = 16
+    if (use_fused && !Q.cols && k > 8 && !x1_store && L >= 64 && nn_tn_supported(L, k)) {
+      const int nb = nt_blocks(L, k);
+      {
+        ProfScope ps(ctx, K_NN_TN, 8.0 * n_local * (L + k) + 8.0 * nb / 2 * L * k);
+        launch_nn_tn(ctx->stream, Q, L, C1, ldc1, X, n_local, partial, nb, sink, false);
+      }
+      ProfScope ps(ctx, K_REDUCE, 8.0 * nb / 2 * L * k);
+      launch_reduce_partials_ld(ctx->stream, partial, nb / 2, L, 8, L, 1.0, out);
+      launch_reduce_partials_ld(ctx->stream, partial + (size_t)(nb / 2) * L * 8, nb / 2, L, k - 8, L, 1.0,
+                                out + (size_t)8 * L);
+      allreduce(out, (size_t)L * k);
+      return false;
+    }
     if (use_fused && fused_wins && !Q.cols && nn_tn_supported(L, k)) {
       const int nb = nt_blocks(L, k);
       {
@@ -560,12 +578,15 @@ struct FastIcgs {
   }
 
   bool gram_ok(int L, int k) const {
-    return gram_on && !slow->dgks && slow->steps == 2 && k >= 2 && k <= 8 && L >= 1 && L <= 1024 && L * k <= 7680;
+    // k <= 8: the closing update carries G1's partials (its LDS holds L x k coefficients);
+    // 9 <= k <= 16: plain closing update, then G1 in a pass of its own (MFMA Gram kernels)
+    return gram_on && !slow->dgks && slow->steps == 2 && k >= 2 && L >= 1 && L <= 1024 &&
+           ((k <= 8 && L * k <= 7680) || (k > 8 && k <= 16));
   }
   void gram_alloc() {
     if (gb.part) return;
-    MIG_HIP(hipMalloc(&gb.part, sizeof(double) * 1024 * 36));
-    MIG_HIP(hipMalloc(&gb.sum, sizeof(double) * 64));
+    MIG_HIP(hipMalloc(&gb.part, sizeof(double) * 1024 * 136));
+    MIG_HIP(hipMalloc(&gb.sum, sizeof(double) * 136));
     MIG_HIP(hipMalloc(&gb.w, sizeof(double) * 768));
   }
   // findBasis in Gram form (icgs.hip): CholQR2 of the block with the reference's dependency
@@ -578,7 +599,11 @@ struct FastIcgs {
     const double gate = gram_gate > 0.0 ? gram_gate : 100.0 * slow->blk_tol;
     auto chol = [&](int stage, int nb) {
       ProfScope ps(ctx, K_REDUCE, 8.0 * nb * nv);
-      if (ctx->nranks > 1) {
+      if (k > 8) {  // block-major partials: fixed-order sum, all-reduce, the k x k step
+        launch_reduce_partials(ctx->stream, gb.part, nb, nv, 1.0, gb.sum);
+        allreduce(gb.sum, (size_t)nv);
+        launch_fbg_chol_l(ctx->stream, gb.sum, k, stage, st, gb.w, gate);
+      } else if (ctx->nranks > 1) {
         launch_fbg_chol(ctx->stream, gb.part, nb, k, 0, st, gb.w, gate, gb.sum);
         allreduce(gb.sum, (size_t)nv);
         launch_fbg_chol(ctx->stream, gb.sum, 1, k, stage, st, gb.w, gate, nullptr);
@@ -682,7 +707,7 @@ struct FastIcgs {
       int nb1 = 0;
       {
         ProfScope ps(ctx, K_GEMM_NN_DOT, 8.0 * n_local * (L + 2.0 * k));
-        if (gram_fuse)
+        if (gram_fuse && k <= 8)
           nb1 = launch_gemm_nn_gram(ctx->stream, qd, L, M2, L, xd, n_local, gb.part);
         else
           launch_gemm_nn(ctx->stream, qd, L, M2, L, xd, n_local, -1.0, 1.0);
@@ -1873,6 +1898,7 @@ extern "C" int migmres_solver_solve(migmres_solver *s, migmres_crs *A, migmres_m
               "LinearProblem: inconsistent X/B/A shapes");
     s->history.clear();
     s->n_apply = s->n_explicit = s->n_restarts = s->n_block_iters = s->n_prec = s->n_deflations = 0;
+    s->fast.gram_calls = s->fast.gram_skips = 0;
     s->t_spmm = s->t_ortho = s->t_lsq = s->t_check = s->t_restart = s->t_setup = 0.0;
     const double comm0 = s->ctx->comm_seconds;
     auto t0 = Clock::now();
@@ -1937,9 +1963,10 @@ extern "C" int migmres_solver_history(const migmres_solver *s, double *out, int 
 }
 extern "C" int migmres_solver_counters(const migmres_solver *s, long long *out, int n) {
   return guard([&] {
-    const long long v[7] = {s->n_apply, s->n_explicit, s->n_restarts, s->ortho.sing_count, s->n_block_iters,
-                            s->n_prec, s->n_deflations};
-    for (int i = 0; i < n && i < 7; ++i) out[i] = v[i];
+    const long long v[9] = {s->n_apply,       s->n_explicit, s->n_restarts,        s->ortho.sing_count,
+                            s->n_block_iters, s->n_prec,     s->n_deflations,      s->fast.gram_calls,
+                            s->fast.gram_skips};
+    for (int i = 0; i < n && i < 9; ++i) out[i] = v[i];
   });
 }
 extern "C" int migmres_solver_timers(const migmres_solver *s, double *out, int n) {
