@@ -155,6 +155,13 @@ int migmres_crs_import_plan(const migmres_crs *A, int *export_lids, int *export_
                             int *remote_lids, int *remote_pids);
 /* OperatorTraits::Apply / Tpetra apply: Y = alpha*A*X + beta*Y (beta==0 ignores Y). */
 int migmres_crs_apply(migmres_crs *A, const migmres_mv *X, migmres_mv *Y, double alpha, double beta);
+/* Which SpMM kernel apply() runs for this operator (chosen at creation from the local rows):
+ * MIGMRES_SPMM_CSR thread per row over the CSR, MIGMRES_SPMM_PAIR row pairs with 16-byte X
+ * loads (rows of <= 8 entries), MIGMRES_SPMM_SELL thread per row over a SELL-64 copy. */
+#define MIGMRES_SPMM_CSR 0
+#define MIGMRES_SPMM_PAIR 1
+#define MIGMRES_SPMM_SELL 2
+int migmres_crs_spmm_kernel(const migmres_crs *A, int *kind);
 
 /* ---------------- multivectors (Belos::MultiVecTraits) ---------------- */
 

@@ -78,6 +78,50 @@ def test_spmm_unstructured_bit_exact(comm, per_row, k, pairs, monkeypatch):
     assert np.array_equal(Yd.download(), Aor.apply(X))
 
 
+def banded_rows(n_global, first, nloc, seed, per_row=20, band=150):
+    """Long rows with locality: per_row random columns within +-band of the row, insertion
+    order random, plus the diagonal."""
+    rng = np.random.default_rng(seed + first)
+    rows, cols, vals = [0], [], []
+    for r in range(nloc):
+        g = first + r
+        lo, hi = max(0, g - band), min(n_global, g + band + 1)
+        c = rng.choice(np.arange(lo, hi), size=min(per_row, hi - lo), replace=False)
+        c = np.concatenate([c[c != g], [g]])
+        cols.extend(c.tolist())
+        vals.extend(rng.standard_normal(len(c)).tolist())
+        rows.append(len(cols))
+    return np.array(rows), np.array(cols), np.array(vals)
+
+
+@pytest.mark.parametrize("kind,k", [("banded", 8), ("banded", 5), ("banded", 1), ("banded", 16), ("Brick3D", 8),
+                                    ("Brick3D", 3), ("Laplace3D", 8)])
+def test_spmm_kernel_choice_bit_exact(comm, kind, k):
+    """Which SpMM kernel an operator gets (migmres_crs_spmm_kernel): the row-pair kernel for
+    7-point rows, the SELL-64 row kernel for 27-point Brick3D rows (config 5) and long banded
+    random rows; bit for bit against the oracle either way."""
+    import trilinos_amd as ta
+    from oracle import epetra as oe
+    if kind == "banded":
+        n = 4099
+        gen = lambda f, m: banded_rows(n, f, m, 31)
+        rp, gc, vv = gen(0, n)
+        A = ta.CrsMatrix(comm, n, rp, gc, vv)
+    else:
+        nx, ny, nz = 13, 12, 11
+        n = nx * ny * nz
+        gen = (lambda f, m: oe.brick3d_rows(nx, ny, nz, f, m)) if kind == "Brick3D" else \
+            (lambda f, m: oe.laplace3d_rows(nx, ny, nz, f, m))
+        A = ta.CrsMatrix.galeri(comm, kind, nx, ny, nz)
+    assert A.spmm_kernel() == ("pair" if kind == "Laplace3D" else "sell")
+    Aor = oe.DistCrs(gen, n, 1)
+    X, _ = oe.epetra_random_mv(13, n, k)
+    Xd = _upload(ta, comm, X)
+    Yd = ta.MultiVector(comm, n, k)
+    A.apply(Xd, Yd)
+    assert np.array_equal(Yd.download(), Aor.apply(X))
+
+
 @pytest.mark.parametrize("n,L,kb", [(1, 1, 1), (63, 5, 3), (64, 16, 16), (1000, 37, 8), (5000, 104, 8),
                                     (4097, 208, 8), (3001, 300, 16), (2049, 600, 20)])
 def test_trans_mv_mfma(comm, n, L, kb):

@@ -915,6 +915,12 @@ void crs_apply(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, double alpha,
 // ------------------------------------------------------------------------------------
 // C ABI: maps, plans, CRS, multivectors
 // ------------------------------------------------------------------------------------
+extern "C" int migmres_crs_spmm_kernel(const migmres_crs *A, int *kind) {
+  return guard([&] {
+    MIG_CHECK(A && kind, "bad arguments");
+    *kind = A->use_pairs ? MIGMRES_SPMM_PAIR : A->use_sell ? MIGMRES_SPMM_SELL : MIGMRES_SPMM_CSR;
+  });
+}
 extern "C" int migmres_map_uniform(long long n_global, int nranks, int rank, long long *first,
                                    int *n_local) {
   return guard([&] {

@@ -157,6 +157,12 @@ class CrsMatrix:
         call("migmres_matrix_file_info", os.fsencode(path), C.byref(ng), None, None)
         return cls(comm, ng.value, _handle=h)
 
+    def spmm_kernel(self):
+        """The SpMM kernel apply() runs: "csr", "pair" or "sell" (migmres_crs_spmm_kernel)."""
+        v = C.c_int()
+        call("migmres_crs_spmm_kernel", self.h, C.byref(v))
+        return ("csr", "pair", "sell")[v.value]
+
     def colmap(self):
         out = np.empty(self.n_cols, dtype=np.int64)
         call("migmres_crs_colmap", self.h, lptr(out))
