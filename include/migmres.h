@@ -241,6 +241,41 @@ int migmres_solver_destroy(migmres_solver *s);
 int migmres_solver_set_int(migmres_solver *s, const char *name, long long value);
 int migmres_solver_set_double(migmres_solver *s, const char *name, double value);
 int migmres_solver_set_string(migmres_solver *s, const char *name, const char *value);
+/* getCurrentParameters (BelosSolverManager.hpp:101): the value in effect, by name and type.
+ * get_string writes at most len bytes including the terminating NUL. */
+int migmres_solver_get_int(const migmres_solver *s, const char *name, long long *value);
+int migmres_solver_get_double(const migmres_solver *s, const char *name, double *value);
+int migmres_solver_get_string(const migmres_solver *s, const char *name, char *value, int len);
+/* getValidParameters / getCurrentParameters (BelosSolverManager.hpp:98-101) as text: one
+ * parameter per line, "name<TAB>type<TAB>value" with type int | bool | double | string;
+ * valid = the solver's defaults (BelosBlockGmresSolMgr.hpp:438-486, pseudo-block
+ * BelosPseudoBlockGmresSolMgr.hpp:494-507), current = the values in effect.  Writes at
+ * most len bytes including the NUL (buf may be NULL to query); *needed = the full size. */
+int migmres_solver_valid_parameters(const migmres_solver *s, char *buf, int len, int *needed);
+int migmres_solver_current_parameters(const migmres_solver *s, char *buf, int len, int *needed);
+/* reset(ResetType) (BelosSolverManager.hpp:177; BlockGmresSolMgr :250 calls setProblem() for
+ * Belos::Problem).  migmres_solver_solve always sets the problem up from the X and B it is
+ * given, so MIGMRES_RESET_PROBLEM only clears the previous solve's results (iterations,
+ * history, counters); MIGMRES_RESET_RECYCLE is accepted and does nothing (GMRES keeps no
+ * recycle space), as in the reference. */
+#define MIGMRES_RESET_PROBLEM 1
+#define MIGMRES_RESET_RECYCLE 2
+int migmres_solver_reset(migmres_solver *s, int type);
+/* setUserConvStatusTest(test, comboType) (BelosSolverManager.hpp:147-155): PseudoBlockGmres
+ * only (BelosPseudoBlockGmresSolMgr.hpp:1070-1078, combined at :1216-1240 as
+ * StatusTestCombo(combo, residual test, user test)); BlockGmresSolMgr does not override it
+ * and the call fails as the reference's throws.  The test is a host callback asked at
+ * every status check with the iteration count and the current right-hand sides' scaled
+ * implicit residual norms (the residual test's testvector); it returns nonzero for
+ * Passed.  Combo: MIGMRES_COMBO_SEQ (the default: the user test is asked only once the
+ * residual test passed), MIGMRES_COMBO_AND (both asked, both must pass), MIGMRES_COMBO_OR
+ * (both asked, either passes).  fn == NULL removes it.  Deflation still follows the residual
+ * test's converged indices, as in the reference. */
+typedef int (*migmres_status_fn)(void *user, int iters, int nrhs, const double *res);
+#define MIGMRES_COMBO_AND 0
+#define MIGMRES_COMBO_OR 1
+#define MIGMRES_COMBO_SEQ 2
+int migmres_solver_set_user_conv_test(migmres_solver *s, migmres_status_fn fn, void *user, int combo);
 /* LinearProblem::setLeftPrec / setRightPrec (BelosLinearProblem.hpp:170-175): side
  * MIGMRES_LEFT_PREC or MIGMRES_RIGHT_PREC; M == NULL removes it.  The solver borrows M. */
 #define MIGMRES_LEFT_PREC 0

@@ -151,3 +151,82 @@ def test_pseudo_parameter_validation(comm):
     sm = ta.PseudoBlockGmresSolMgr(lp, {"Block Size": 2, "Deflation Quorum": 3})
     with pytest.raises(MigmresError):
         sm.solve()
+
+
+def test_solver_manager_parameter_lists_and_reset(comm):
+    """getValidParameters / getCurrentParameters / reset through the C ABI
+    (BelosSolverManager.hpp:98-101, 177): the valid list is the reference's defaults, the
+    current list follows setParameters, reset(Problem) clears the previous solve's results."""
+    import trilinos_amd as ta
+    from trilinos_amd._lib import MigmresError
+    from trilinos_amd.belos import DEFAULT_PARAMETERS, PSEUDO_DEFAULT_PARAMETERS
+    n, gen, Xe = _problem("Laplace2D", (12, 11, 1), 2)
+    A = ta.CrsMatrix.galeri(comm, "Laplace2D", 12, 11)
+    for cls, defaults in ((ta.BlockGmresSolMgr, DEFAULT_PARAMETERS),
+                          (ta.PseudoBlockGmresSolMgr, PSEUDO_DEFAULT_PARAMETERS)):
+        Xd, B = ta.MultiVector(comm, n, 2), ta.MultiVector(comm, n, 2)
+        Xv = ta.MultiVector(comm, n, 2)
+        Xv.upload(Xe)
+        A.apply(Xv, B)
+        Xd.put_scalar(0.0)
+        lp = ta.LinearProblem(A, Xd, B)
+        lp.setProblem()
+        sm = cls(lp, {"Block Size": 2, "Num Blocks": 7, "Convergence Tolerance": 1e-7,
+                      "Orthogonalization": "ICGS"})
+        sm._ensure()
+        assert sm.getValidParameters() == defaults
+        cur = sm.getCurrentParameters()
+        assert cur == dict(defaults, **{"Block Size": 2, "Num Blocks": 7, "Convergence Tolerance": 1e-7,
+                                        "Orthogonalization": "ICGS"})
+        assert sm.solve() == ta.Converged and sm.getNumIters() > 0
+        sm.reset(1)
+        assert sm.getNumIters() == 0 and sm.residualHistory().size == 0
+        assert sm.counters()["applies"] == 0
+        with pytest.raises(MigmresError):
+            sm.reset(4)
+
+
+def test_user_conv_status_test(comm):
+    """setUserConvStatusTest (pseudo-block only, BelosPseudoBlockGmresSolMgr.hpp:1070-1078,
+    combined with the residual test at :1216-1240): SEQ with an always-passing test = no user
+    test; SEQ that passes only from a later iteration on delays convergence to it; AND with a
+    never-passing test runs to Maximum Iterations; BlockGmresSolMgr refuses, as the reference's
+    base class throws."""
+    import trilinos_amd as ta
+    from trilinos_amd._lib import MigmresError
+    n, gen, Xe = _problem("Laplace2D", (14, 13, 1), 2)
+    params = {"Block Size": 2, "Num Blocks": 200, "Maximum Iterations": 200, "Convergence Tolerance": 1e-6}
+
+    def run(test, combo):
+        A = ta.CrsMatrix.galeri(comm, "Laplace2D", 14, 13)
+        Xv, B, X = ta.MultiVector(comm, n, 2), ta.MultiVector(comm, n, 2), ta.MultiVector(comm, n, 2)
+        Xv.upload(Xe)
+        A.apply(Xv, B)
+        X.put_scalar(0.0)
+        lp = ta.LinearProblem(A, X, B)
+        lp.setProblem()
+        sm = ta.PseudoBlockGmresSolMgr(lp, params)
+        seen = []
+        if test is not None:
+            sm.setUserConvStatusTest(lambda it, res: (seen.append((it, res.copy())), test(it, res))[1], combo)
+        ret = sm.solve()
+        return ret, sm.getNumIters(), sm.residualHistory(), seen
+
+    ret0, it0, h0, _ = run(None, "SEQ")
+    assert ret0 == ta.Converged and it0 + 30 < params["Maximum Iterations"]
+    ret1, it1, h1, seen1 = run(lambda it, res: True, "SEQ")
+    assert (ret1, it1) == (ret0, it0) and np.array_equal(h1, h0)
+    # SEQ: the user test is asked only once the residual test passed (some column converged)
+    assert seen1 and all(np.any(r <= 1e-6) for _, r in seen1)
+    late = it0 + 10
+    ret2, it2, _, _ = run(lambda it, res: it >= late, "SEQ")
+    assert ret2 == ta.Converged and it2 == late
+    params["Maximum Iterations"] = it0 + 20
+    ret3, it3, _, seen3 = run(lambda it, res: False, "AND")
+    assert ret3 == ta.Unconverged and it3 == params["Maximum Iterations"] and len(seen3) >= it3
+    A = ta.CrsMatrix.galeri(comm, "Laplace2D", 14, 13)
+    lp = ta.LinearProblem(A, ta.MultiVector(comm, n, 2), ta.MultiVector(comm, n, 2))
+    lp.setProblem()
+    sm = ta.BlockGmresSolMgr(lp, params)
+    with pytest.raises(MigmresError):
+        sm.setUserConvStatusTest(lambda it, res: True)

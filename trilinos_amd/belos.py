@@ -268,7 +268,40 @@ class BlockGmresSolMgr:
         self.problem = problem
 
     def getValidParameters(self):
+        if self.h is not None:
+            return self._abi_params("migmres_solver_valid_parameters")
         return dict(self._defaults)
+
+    def _abi_params(self, fn):
+        """The library's parameter list text ("name\ttype\tvalue" lines) as a dict."""
+        need = C.c_int()
+        call(fn, self.h, None, 0, C.byref(need))
+        buf = C.create_string_buffer(need.value)
+        call(fn, self.h, buf, need.value, C.byref(need))
+        out = {}
+        for line in buf.value.decode().splitlines():
+            name, typ, val = line.split("\t")
+            out[name] = (int(val) if typ == "int" else val == "true" if typ == "bool"
+                         else float(val) if typ == "double" else val)
+        return out
+
+    def reset(self, type=1):
+        """SolverManager::reset(ResetType): 1 = Belos::Problem, 2 = Belos::RecycleSubspace."""
+        self._ensure()
+        call("migmres_solver_reset", self.h, int(type))
+
+    def setUserConvStatusTest(self, test, comboType="SEQ"):
+        """StatusTestCombo(comboType, residual test, test) -- pseudo-block GMRES only, as in the
+        reference.  test(iters, res) -> bool, res = the scaled implicit residual norms."""
+        self._ensure()
+        combo = {"AND": 0, "OR": 1, "SEQ": 2}[comboType]
+        if test is None:
+            self._user_cb = None
+            call("migmres_solver_set_user_conv_test", self.h, None, None, combo)
+            return
+        proto = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_double))
+        self._user_cb = proto(lambda _u, it, n, r: 1 if test(it, np.ctypeslib.as_array(r, (n,)).copy()) else 0)
+        call("migmres_solver_set_user_conv_test", self.h, self._user_cb, None, combo)
 
     def setParameters(self, params):
         for k, v in params.items():
@@ -287,6 +320,8 @@ class BlockGmresSolMgr:
                 self._push(k, v)
 
     def getCurrentParameters(self):
+        if self.h is not None:
+            return self._abi_params("migmres_solver_current_parameters")
         return dict(self.params)
 
     def solve(self):

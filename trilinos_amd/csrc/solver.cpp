@@ -832,6 +832,10 @@ struct migmres_solver {
   bool loa = false;
   std::vector<double> history;
   int hist_cols = 0;
+  // setUserConvStatusTest (pseudo-block only)
+  migmres_status_fn user_test = nullptr;
+  void *user_data = nullptr;
+  int user_combo = MIGMRES_COMBO_SEQ;
   long long n_apply = 0, n_explicit = 0, n_restarts = 0, n_block_iters = 0, n_prec = 0, n_deflations = 0;
   double t_total = 0, t_spmm = 0, t_ortho = 0, t_lsq = 0, t_comm = 0;
   double t_check = 0, t_restart = 0, t_setup = 0;
@@ -1596,6 +1600,17 @@ struct PseudoEngine : Engine {
       conv_passed = res_check(imp, nat, upd);
     else
       conv_passed = res_check(imp, nat, upd) && res_check(exp, nat, upd);
+    if (S->user_test) {  // StatusTestCombo(combo, residual test, user test) (:1216-1240)
+      auto user = [&] {
+        return S->user_test(S->user_data, it.num_iters, (int)imp.testvector.size(), imp.testvector.data()) != 0;
+      };
+      if (S->user_combo == MIGMRES_COMBO_SEQ)
+        conv_passed = conv_passed && user();
+      else if (S->user_combo == MIGMRES_COMBO_AND)
+        conv_passed = user() && conv_passed;
+      else
+        conv_passed = user() || conv_passed;
+    }
     S->history.insert(S->history.end(), imp.testvector.begin(), imp.testvector.end());
     S->hist_cols = (int)imp.testvector.size();
     S->t_check += since(t0);
@@ -1886,6 +1901,131 @@ extern "C" int migmres_solver_set_string(migmres_solver *s, const char *name, co
     } else {
       throw Error(MIGMRES_EINVAL, "unknown string parameter \"" + n + "\"");
     }
+  });
+}
+
+namespace {
+// the parameter list of a solver (names/types of BelosBlockGmresSolMgr.hpp:438-486 and
+// BelosPseudoBlockGmresSolMgr.hpp:494-507) as "name\ttype\tvalue" lines
+std::string param_text(const Params &p) {
+  std::string out;
+  char num[64];
+  auto line = [&](const char *name, const char *type, const std::string &v) {
+    out += name;
+    out += '\t';
+    out += type;
+    out += '\t';
+    out += v;
+    out += '\n';
+  };
+  auto i = [&](const char *name, long long v) {
+    std::snprintf(num, sizeof num, "%lld", v);
+    line(name, "int", num);
+  };
+  auto b = [&](const char *name, bool v) { line(name, "bool", v ? "true" : "false"); };
+  std::snprintf(num, sizeof num, "%.17g", p.tol);
+  line("Convergence Tolerance", "double", num);
+  i("Maximum Restarts", p.max_restarts);
+  i("Maximum Iterations", p.max_iters);
+  i("Num Blocks", p.num_blocks);
+  i("Block Size", p.block_size);
+  if (!p.pseudo) b("Adaptive Block Size", p.adaptive);
+  i("Verbosity", p.verbosity);
+  i("Output Frequency", p.output_freq);
+  if (p.pseudo) i("Deflation Quorum", p.def_quorum);
+  line("Orthogonalization", "string", p.ortho);
+  if (!p.pseudo) b("Flexible Gmres", p.flexible);
+  b("Explicit Residual Test", p.exp_res_test);
+  line("Implicit Residual Scaling", "string", p.imp_scale);
+  line("Explicit Residual Scaling", "string", p.exp_scale);
+  return out;
+}
+void put_text(const std::string &t, char *buf, int len, int *needed) {
+  if (needed) *needed = (int)t.size() + 1;
+  if (buf && len > 0) {
+    const size_t n = std::min(t.size(), (size_t)len - 1);
+    std::memcpy(buf, t.data(), n);
+    buf[n] = '\0';
+  }
+}
+}  // namespace
+
+extern "C" int migmres_solver_valid_parameters(const migmres_solver *s, char *buf, int len, int *needed) {
+  return guard([&] {
+    MIG_CHECK(s, "bad arguments");
+    Params d;
+    d.pseudo = s->p.pseudo;
+    if (d.pseudo) d.ortho = "ICGS";  // BelosPseudoBlockGmresSolMgr.hpp:506
+    put_text(param_text(d), buf, len, needed);
+  });
+}
+extern "C" int migmres_solver_current_parameters(const migmres_solver *s, char *buf, int len, int *needed) {
+  return guard([&] {
+    MIG_CHECK(s, "bad arguments");
+    put_text(param_text(s->p), buf, len, needed);
+  });
+}
+extern "C" int migmres_solver_get_int(const migmres_solver *s, const char *name, long long *v) {
+  return guard([&] {
+    MIG_CHECK(s && name && v, "bad arguments");
+    const std::string n(name);
+    const Params &p = s->p;
+    if (n == "Block Size") *v = p.block_size;
+    else if (n == "Num Blocks") *v = p.num_blocks;
+    else if (n == "Maximum Iterations") *v = p.max_iters;
+    else if (n == "Maximum Restarts") *v = p.max_restarts;
+    else if (n == "Adaptive Block Size" && !p.pseudo) *v = p.adaptive;
+    else if (n == "Flexible Gmres" && !p.pseudo) *v = p.flexible;
+    else if (n == "Deflation Quorum" && p.pseudo) *v = p.def_quorum;
+    else if (n == "Explicit Residual Test") *v = p.exp_res_test;
+    else if (n == "Verbosity") *v = p.verbosity;
+    else if (n == "Output Frequency") *v = p.output_freq;
+    else throw Error(MIGMRES_EINVAL, "unknown integer parameter \"" + n + "\"");
+  });
+}
+extern "C" int migmres_solver_get_double(const migmres_solver *s, const char *name, double *v) {
+  return guard([&] {
+    MIG_CHECK(s && name && v, "bad arguments");
+    MIG_CHECK(std::string(name) == "Convergence Tolerance", "unknown double parameter \"" + std::string(name) + "\"");
+    *v = s->p.tol;
+  });
+}
+extern "C" int migmres_solver_get_string(const migmres_solver *s, const char *name, char *v, int len) {
+  return guard([&] {
+    MIG_CHECK(s && name && v && len > 0, "bad arguments");
+    const std::string n(name);
+    const std::string &val = n == "Orthogonalization" ? s->p.ortho
+                             : n == "Implicit Residual Scaling" ? s->p.imp_scale
+                             : n == "Explicit Residual Scaling" ? s->p.exp_scale
+                             : throw Error(MIGMRES_EINVAL, "unknown string parameter \"" + n + "\"");
+    put_text(val, v, len, nullptr);
+  });
+}
+extern "C" int migmres_solver_reset(migmres_solver *s, int type) {
+  return guard([&] {
+    MIG_CHECK(s, "bad arguments");
+    MIG_CHECK((type & ~(MIGMRES_RESET_PROBLEM | MIGMRES_RESET_RECYCLE)) == 0, "reset: unknown ResetType bits");
+    if (type & MIGMRES_RESET_PROBLEM) {
+      s->num_iters = 0;
+      s->achieved_tol = 0.0;
+      s->loa = false;
+      s->history.clear();
+      s->hist_cols = 0;
+      s->n_apply = s->n_explicit = s->n_restarts = s->n_block_iters = s->n_prec = s->n_deflations = 0;
+      s->fast.gram_calls = s->fast.gram_skips = 0;
+    }
+  });
+}
+extern "C" int migmres_solver_set_user_conv_test(migmres_solver *s, migmres_status_fn fn, void *user, int combo) {
+  return guard([&] {
+    MIG_CHECK(s, "bad arguments");
+    MIG_CHECK(s->p.pseudo, "setUserConvStatusTest() has not been overridden for BlockGmresSolMgr "
+                           "(BelosSolverManager.hpp:147-155); use the pseudo-block solver");
+    MIG_CHECK(combo == MIGMRES_COMBO_AND || combo == MIGMRES_COMBO_OR || combo == MIGMRES_COMBO_SEQ,
+              "combo must be MIGMRES_COMBO_AND, _OR or _SEQ");
+    s->user_test = fn;
+    s->user_data = user;
+    s->user_combo = combo;
   });
 }
 
