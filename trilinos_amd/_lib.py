@@ -24,6 +24,9 @@ i64 = C.c_longlong
 f64 = C.c_double
 P = C.POINTER
 
+# setUserConvStatusTest callback: (user, iters, nrhs, scaled residual norms) -> passed
+STATUS_FN = C.CFUNCTYPE(i32, vp, i32, i32, P(f64))
+
 # name: (argtypes)
 _SIGS = {
     "migmres_abi_version": [],
@@ -50,6 +53,7 @@ _SIGS = {
     "migmres_crs_colmap": [vp, P(i64)],
     "migmres_crs_import_plan": [vp, P(i32), P(i32), P(i32), P(i32)],
     "migmres_crs_apply": [vp, vp, vp, f64, f64],
+    "migmres_crs_spmm_kernel": [vp, P(i32)],
     "migmres_mv_create": [vp, i64, i32, i32, P(vp)],
     "migmres_mv_view": [vp, P(i32), i32, P(vp)],
     "migmres_mv_view_range": [vp, i32, i32, P(vp)],
@@ -84,6 +88,13 @@ _SIGS = {
     "migmres_solver_set_int": [vp, C.c_char_p, i64],
     "migmres_solver_set_double": [vp, C.c_char_p, f64],
     "migmres_solver_set_string": [vp, C.c_char_p, C.c_char_p],
+    "migmres_solver_get_int": [vp, C.c_char_p, P(i64)],
+    "migmres_solver_get_double": [vp, C.c_char_p, P(f64)],
+    "migmres_solver_get_string": [vp, C.c_char_p, C.c_char_p, i32],
+    "migmres_solver_valid_parameters": [vp, C.c_char_p, i32, P(i32)],
+    "migmres_solver_current_parameters": [vp, C.c_char_p, i32, P(i32)],
+    "migmres_solver_reset": [vp, i32],
+    "migmres_solver_set_user_conv_test": [vp, STATUS_FN, vp, i32],
     "migmres_solver_solve": [vp, vp, vp, vp, P(i32)],
     "migmres_solver_num_iters": [vp, P(i32)],
     "migmres_solver_achieved_tol": [vp, P(f64)],

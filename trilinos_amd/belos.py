@@ -16,7 +16,7 @@ import ctypes as C
 
 import numpy as np
 
-from ._lib import call, dptr, iptr
+from ._lib import STATUS_FN, call, dptr, iptr
 from .linalg import MultiVector, TWO_NORM, ONE_NORM, INF_NORM  # noqa: F401
 
 Converged, Unconverged = "Converged", "Unconverged"  # Belos::ReturnType (BelosTypes.hpp:155-157)
@@ -299,8 +299,7 @@ class BlockGmresSolMgr:
             self._user_cb = None
             call("migmres_solver_set_user_conv_test", self.h, None, None, combo)
             return
-        proto = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_double))
-        self._user_cb = proto(lambda _u, it, n, r: 1 if test(it, np.ctypeslib.as_array(r, (n,)).copy()) else 0)
+        self._user_cb = STATUS_FN(lambda _u, it, n, r: 1 if test(it, np.ctypeslib.as_array(r, (n,)).copy()) else 0)
         call("migmres_solver_set_user_conv_test", self.h, self._user_cb, None, combo)
 
     def setParameters(self, params):
