@@ -389,7 +389,6 @@ struct FastIcgs {
     pbuf[0] = partial;
     MIG_HIP(hipMalloc(&pbuf[1], sizeof(double) * (size_t)nblk_ic * 17));
     MIG_HIP(hipHostMalloc(&h, sizeof(IcgsState) + sizeof(double) * (size_t)(lmax + k) * k, hipHostMallocDefault));
-    tmpX = MvPtr(mv_create(c, ng, nl, k));
   }
 
   void allreduce(double *d, size_t n) {
@@ -645,6 +644,7 @@ struct FastIcgs {
   const double *hC() const { return h + sizeof(IcgsState) / sizeof(double); }
 
   void save_input(migmres_mv &X) {
+    if (!tmpX.p) tmpX = MvPtr(mv_create(ctx, n_global, n_local, kmax));  // first use
     ProfScope ps(ctx, K_COPY, 16.0 * n_local * X.ncols);
     MvPtr t = view(*tmpX, 0, X.ncols);
     launch_copy(ctx->stream, X.desc(), t->desc(), n_local);
@@ -668,20 +668,9 @@ struct FastIcgs {
     launch_state_reset(ctx->stream, st, slow->blk_tol, slow->sing_tol, slow->dgks ? 1 : 0, slow->dep_tol);
     const MvDesc xd = X.desc(), qd = Q.desc();
     if (k == 1) {  // blkOrtho1, then MvDot and MvScale
-      tn(qd, L, xd, 1, R1, L);
-      const bool x1 = nn_then_tn(qd, L, R1, L, xd, 1, R2);
-      launch_add_coef(ctx->stream, R1, L, R2, L, Cout, L, L, 1);
-      nn(qd, L, x1 ? R2 : Cout, L, xd, 1, 1);
-      set_pending(pbuf[0], 1, 4, -1, 0, 1, 0);
-      {
-        ProfScope ps(ctx, K_SCALE, 16.0 * n_local);
-        const FbPro pro = take_pending();
-        launch_scale_col(ctx->stream, xd, 0, pro, n_local, nblk_ic);
-      }
+      enqueue_k1(X, Q);
       fetch(L, 1);
-      for (int i = 0; i < L; ++i) C[i] = hC()[i];
-      B[0] = hst().B[0];
-      return 1;
+      return result_k1(L, C, B);
     }
     if (!regen) save_input(X);
     // blkOrtho: oldDot comes from the Gram block of [Q X]^T X when Q and X are adjacent
@@ -746,6 +735,37 @@ struct FastIcgs {
       for (int i = 0; i < k; ++i) B[i + (size_t)j * ldb] = s.B[i + 16 * j];
     }
     return k;
+  }
+
+  // The k == 1 projectAndNormalize as a kernel chain ending in the D2H copy of the state
+  // and coefficients, without the wait: PseudoBlockGmres enqueues every right-hand side's
+  // chain (one FastIcgs each) and waits once (fetch_async / result_k1).
+  void enqueue_k1(migmres_mv &X, migmres_mv &Q) {
+    const int L = Q.ncols;
+    ++calls;
+    pend = Pending{};
+    launch_state_reset(ctx->stream, st, slow->blk_tol, slow->sing_tol, slow->dgks ? 1 : 0, slow->dep_tol);
+    const MvDesc xd = X.desc(), qd = Q.desc();
+    tn(qd, L, xd, 1, R1, L);
+    const bool x1 = nn_then_tn(qd, L, R1, L, xd, 1, R2);
+    launch_add_coef(ctx->stream, R1, L, R2, L, Cout, L, L, 1);
+    nn(qd, L, x1 ? R2 : Cout, L, xd, 1, 1);
+    set_pending(pbuf[0], 1, 4, -1, 0, 1, 0);
+    ProfScope ps(ctx, K_SCALE, 16.0 * n_local);
+    const FbPro pro = take_pending();
+    launch_scale_col(ctx->stream, xd, 0, pro, n_local, nblk_ic);
+  }
+  void fetch_async(int L, int k) {
+    flush_pending();
+    MIG_HIP(hipMemcpyAsync(h, st, sizeof(IcgsState), hipMemcpyDeviceToHost, ctx->stream));
+    if (L > 0)
+      MIG_HIP(hipMemcpyAsync(h + sizeof(IcgsState) / sizeof(double), Cout, sizeof(double) * (size_t)L * k,
+                             hipMemcpyDeviceToHost, ctx->stream));
+  }
+  int result_k1(int L, double *C, double *B) const {
+    for (int i = 0; i < L; ++i) C[i] = hC()[i];
+    B[0] = hst().B[0];
+    return 1;
   }
 
   // normalize = findBasis(completeBasis = true)
@@ -1557,6 +1577,21 @@ struct PseudoIter {
 struct PseudoEngine : Engine {
   PseudoEngine(migmres_solver *s, double tol, int mi) : Engine(s, tol, mi) {}
 
+  // One device ICGS state per right-hand side slot (ICGS; DGKS's k = 1 blkOrtho1 decides its
+  // second pass on the host between the passes and keeps the host path).
+  std::vector<std::unique_ptr<FastIcgs>> rhs_fast;
+  int rhs_nb = 0;
+  bool device_ortho() const { return S->use_fast && !S->ortho.dgks && S->ortho.steps == 2; }
+  FastIcgs &rhs_ortho(int slot) {
+    auto &f = rhs_fast[(size_t)slot];
+    if (!f) {
+      f.reset(new FastIcgs());
+      f->slow = &S->ortho;
+      f->setup(lp.X->ctx, lp.X->n_global, lp.X->n_local, 1, rhs_nb + 1);
+    }
+    return *f;
+  }
+
   void setup_pseudo_tests(bool has_left) {  // checkStatusTest (:1156-1265)
     seq = S->p.exp_res_test || has_left;
     imp.kind = seq ? ResTest::GEN_IMPLICIT : ResTest::IMP_RES_NORM;
@@ -1636,13 +1671,35 @@ struct PseudoEngine : Engine {
       lp.apply(*U, *AU);
       auto t0 = Clock::now();
       h.assign((size_t)c + 1, 0.0);
-      for (int i = 0; i < n; ++i) {
-        PseudoRhs &rs = it.st[(size_t)i];
-        MvPtr w = view(*it.V, vcols[(size_t)i], 1);
-        MvPtr Q = view(*it.V, it.col(rs, 0), c + 1);
-        S->ortho.project_and_normalize(*w, *Q, h.data(), c + 1, r.data(), 1);
-        for (int q = 0; q <= c; ++q) it.Hat(rs, q, c) = h[(size_t)q];
-        it.Hat(rs, c + 1, c) = r[0];
+      if (device_ortho()) {
+        // every right-hand side's ICGS chain on the stream (its own FastIcgs state), one wait
+        std::vector<MvPtr> ws, qs;
+        for (int i = 0; i < n; ++i) {
+          PseudoRhs &rs = it.st[(size_t)i];
+          ws.push_back(view(*it.V, vcols[(size_t)i], 1));
+          qs.push_back(view(*it.V, it.col(rs, 0), c + 1));
+          FastIcgs &f = rhs_ortho(rs.slot);
+          f.enqueue_k1(*ws.back(), *qs.back());
+          f.fetch_async(c + 1, 1);
+        }
+        MIG_HIP(hipStreamSynchronize(lp.X->ctx->stream));
+        for (int i = 0; i < n; ++i) {
+          PseudoRhs &rs = it.st[(size_t)i];
+          const FastIcgs &f = rhs_ortho(rs.slot);
+          if (f.hst().neg != 0.0) throw Error(MIGMRES_ESTATE, "ICGS: negative definiteness in inner product");
+          f.result_k1(c + 1, h.data(), r.data());
+          for (int q = 0; q <= c; ++q) it.Hat(rs, q, c) = h[(size_t)q];
+          it.Hat(rs, c + 1, c) = r[0];
+        }
+      } else {
+        for (int i = 0; i < n; ++i) {
+          PseudoRhs &rs = it.st[(size_t)i];
+          MvPtr w = view(*it.V, vcols[(size_t)i], 1);
+          MvPtr Q = view(*it.V, it.col(rs, 0), c + 1);
+          S->ortho.project_and_normalize(*w, *Q, h.data(), c + 1, r.data(), 1);
+          for (int q = 0; q <= c; ++q) it.Hat(rs, q, c) = h[(size_t)q];
+          it.Hat(rs, c + 1, c) = r[0];
+        }
       }
       S->t_ortho += since(t0);
       update_lsqr(it);
@@ -1705,6 +1762,9 @@ struct PseudoEngine : Engine {
     PseudoIter it;
     it.nb = p.num_blocks;
     it.V = MvPtr(mv_create(lp.X->ctx, lp.X->n_global, lp.X->n_local, block * (p.num_blocks + 1)));
+    rhs_nb = p.num_blocks;
+    rhs_fast.clear();
+    rhs_fast.resize((size_t)block);
     while (to_solve > 0) {
       auto ts0 = Clock::now();
       std::vector<int> cur_idx(idx.begin(), idx.begin() + cur);
