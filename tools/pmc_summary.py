@@ -27,7 +27,8 @@ KMAP = {"k_gemm_tn": ("gemm_tn", True), "k_gemm_nn": ("gemm_nn", True),
         "k_spmm": ("spmm", False), "k_spmm_pair": ("spmm", False),
         "k_fb_a": ("findbasis", True), "k_fb_a01": ("findbasis", True), "k_fb_b2": ("findbasis", True),
         "k_fb_ca": ("findbasis", True), "k_gemm_nn_gram": ("gemm_nn_dot", True),
-        "k_fbg_gram": ("findbasis", True), "k_fbg_a": ("findbasis", True), "k_fbg_b": ("findbasis", True)}
+        "k_fbg_gram": ("findbasis", True), "k_fbg_a": ("findbasis", True), "k_fbg_b": ("findbasis", True),
+        "k_fbg_gram_m": ("findbasis", False), "k_fbg_b_m": ("findbasis", False)}
 
 
 def base(name):
