@@ -110,6 +110,15 @@ int migmres_plan_local_crs(long long first, int n_local, const long long *rowptr
  * does not fit the plan and the row-per-thread kernel is used instead). */
 int migmres_plan_pairs(int n_local, const long long *rowptr, const int *xcols, int *ptr_out,
                        int *key_out, unsigned short *meta_out, long long *nkeys, int *ok);
+/* The row-pair template form of the same X-space CSR (k_spmm_tpl): per pair a template id
+ * (255: the pair reads a ghost column), per template maxk key records (offset from the pair,
+ * four value-dictionary slots packed in bytes: row 0 low, row 0 high, row 1 low, row 1 high,
+ * 255 = none) and the value dictionary.  *ok = 0 when the rows do not repeat few enough
+ * shapes.  Pass null outputs to get the sizes: id (n_local+1)/2 bytes, rec 2*ntpl*maxk ints,
+ * vals nvals doubles. */
+int migmres_plan_pair_templates(int n_local, const long long *rowptr, const int *xcols, const double *vals,
+                                unsigned char *id_out, int *rec_out, double *vals_out, int *ntpl, int *maxk,
+                                int *nvals, int *ok);
 
 /* ---------------- CRS operator (Epetra_CrsMatrix / Tpetra::CrsMatrix) ---------------- */
 
@@ -157,10 +166,15 @@ int migmres_crs_import_plan(const migmres_crs *A, int *export_lids, int *export_
 int migmres_crs_apply(migmres_crs *A, const migmres_mv *X, migmres_mv *Y, double alpha, double beta);
 /* Which SpMM kernel apply() runs for this operator (chosen at creation from the local rows):
  * MIGMRES_SPMM_CSR thread per row over the CSR, MIGMRES_SPMM_PAIR row pairs with 16-byte X
- * loads (rows of <= 8 entries), MIGMRES_SPMM_SELL thread per row over a SELL-64 copy. */
+ * loads (rows of <= 8 entries), MIGMRES_SPMM_SELL thread per row over a SELL-64 copy,
+ * MIGMRES_SPMM_TPL row pairs read through a few repeated pair templates (one byte per pair;
+ * stencil operators), the pairs that read ghost columns through one of the others.
+ * MIGMRES_NO_TPL_SPMM=1 / MIGMRES_NO_PAIR_SPMM=1 / MIGMRES_NO_SELL_SPMM=1 in the environment
+ * at creation switch the respective format off.  Every kernel is bit-identical. */
 #define MIGMRES_SPMM_CSR 0
 #define MIGMRES_SPMM_PAIR 1
 #define MIGMRES_SPMM_SELL 2
+#define MIGMRES_SPMM_TPL 3
 int migmres_crs_spmm_kernel(const migmres_crs *A, int *kind);
 
 /* ---------------- multivectors (Belos::MultiVecTraits) ---------------- */

@@ -94,14 +94,20 @@ def banded_rows(n_global, first, nloc, seed, per_row=20, band=150):
     return np.array(rows), np.array(cols), np.array(vals)
 
 
-@pytest.mark.parametrize("kind,k", [("banded", 8), ("banded", 5), ("banded", 1), ("banded", 16), ("Brick3D", 8),
-                                    ("Brick3D", 3), ("Laplace3D", 8)])
-def test_spmm_kernel_choice_bit_exact(comm, kind, k):
-    """Which SpMM kernel an operator gets (migmres_crs_spmm_kernel): the row-pair kernel for
-    7-point rows, the SELL-64 row kernel for 27-point Brick3D rows (config 5) and long banded
-    random rows; bit for bit against the oracle either way."""
+@pytest.mark.parametrize("kind,k,tpl", [("banded", 8, True), ("banded", 5, True), ("banded", 1, True),
+                                        ("banded", 16, True), ("Brick3D", 8, True), ("Brick3D", 3, True),
+                                        ("Brick3D", 16, True), ("Laplace3D", 8, True), ("Laplace3D", 5, True),
+                                        ("Brick3D", 8, False), ("Laplace3D", 8, False)])
+def test_spmm_kernel_choice_bit_exact(comm, kind, k, tpl, monkeypatch):
+    """Which SpMM kernel an operator gets (migmres_crs_spmm_kernel): the row-pair template
+    kernel for stencils (7-point and 27-point: one byte per row pair), otherwise -- or with
+    MIGMRES_NO_TPL_SPMM=1 -- the row-pair kernel for 7-point rows, the SELL-64 row kernel for
+    27-point Brick3D rows (config 5) and long banded random rows; bit for bit against the
+    oracle either way."""
     import trilinos_amd as ta
     from oracle import epetra as oe
+    if not tpl:
+        monkeypatch.setenv("MIGMRES_NO_TPL_SPMM", "1")
     if kind == "banded":
         n = 4099
         gen = lambda f, m: banded_rows(n, f, m, 31)
@@ -113,7 +119,10 @@ def test_spmm_kernel_choice_bit_exact(comm, kind, k):
         gen = (lambda f, m: oe.brick3d_rows(nx, ny, nz, f, m)) if kind == "Brick3D" else \
             (lambda f, m: oe.laplace3d_rows(nx, ny, nz, f, m))
         A = ta.CrsMatrix.galeri(comm, kind, nx, ny, nz)
-    assert A.spmm_kernel() == ("pair" if kind == "Laplace3D" else "sell")
+    if tpl and kind != "banded":
+        assert A.spmm_kernel() == "tpl"
+    else:
+        assert A.spmm_kernel() == ("pair" if kind == "Laplace3D" else "sell")
     Aor = oe.DistCrs(gen, n, 1)
     X, _ = oe.epetra_random_mv(13, n, k)
     Xd = _upload(ta, comm, X)

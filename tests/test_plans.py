@@ -219,3 +219,96 @@ def test_pair_plan_rejects_long_rows_and_repeats():
     ptr, key, meta = lib_pair_plan(3, rp, xc)
     seq = replay_pair_plan(3, ptr, key, meta)
     assert seq == [[(0, 0), (1, 2)], [(0, 1)], [(0, 0), (1, 2)]]
+
+
+def lib_pair_templates(nloc, rowptr, xcols, vals):
+    L = _lib()
+    rowptr = np.ascontiguousarray(rowptr, dtype=np.int64)
+    xcols = np.ascontiguousarray(xcols, dtype=np.int32)
+    vals = np.ascontiguousarray(vals, dtype=np.float64)
+    nt, mk, nv, ok = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+    args = (nloc, L.lptr(rowptr), L.iptr(xcols), vals.ctypes.data_as(C.POINTER(C.c_double)))
+    L.call("migmres_plan_pair_templates", *args, None, None, None, C.byref(nt), C.byref(mk), C.byref(nv),
+           C.byref(ok))
+    if not ok.value:
+        return None
+    tid = np.empty((nloc + 1) // 2, dtype=np.uint8)
+    rec = np.empty(2 * nt.value * mk.value, dtype=np.int32)
+    dic = np.empty(max(nv.value, 1), dtype=np.float64)
+    L.call("migmres_plan_pair_templates", *args, tid.ctypes.data_as(C.POINTER(C.c_uint8)), L.iptr(rec),
+           dic.ctypes.data_as(C.POINTER(C.c_double)), C.byref(nt), C.byref(mk), C.byref(nv), C.byref(ok))
+    return tid, rec.reshape(nt.value, mk.value, 2), dic[:nv.value]
+
+
+def replay_pair_templates(nloc, tid, rec, dic):
+    """Per row, the (value, X-space column) sequence k_spmm_tpl adds: the pair's template keys
+    in order, low half before high half, coefficient from the value dictionary."""
+    seq = [[] for _ in range(nloc)]
+    for p, t in enumerate(tid.tolist()):
+        if t == 255:
+            continue
+        for off, slots in rec[t].tolist():
+            for h in range(2):
+                for half in range(2):
+                    s = (slots >> (8 * (2 * h + half))) & 0xFF
+                    if s == 0xFF:
+                        continue
+                    assert 2 * p + h < nloc
+                    seq[2 * p + h].append((dic[s], 2 * (p + off) + half))
+    return seq
+
+
+@pytest.mark.parametrize("kind,dims,P", [("Laplace2D", (100, 100, 1), 1), ("Laplace3D", (16, 12, 10), 1),
+                                         ("Laplace3D", (9, 7, 5), 1), ("Brick3D", (13, 12, 11), 1),
+                                         ("Laplace3D", (16, 12, 10), 3), ("Brick3D", (13, 12, 11), 2)])
+def test_pair_templates_replay_stored_order(kind, dims, P):
+    """The template SpMM plan (one byte per row pair) reproduces every templated row's
+    entries -- value bit patterns and X-space columns -- in stored order, so k_spmm_tpl's
+    sums are the reference's bit for bit; exactly the pairs that read a ghost column are
+    left to the fallback kernel; a stencil needs a few dozen templates."""
+    nx, ny, nz = dims
+    n_global = nx * ny * (nz if kind != "Laplace2D" else 1)
+    gen = {"Laplace2D": lambda f, m: oe.laplace2d_rows(nx, ny, f, m),
+           "Laplace3D": lambda f, m: oe.laplace3d_rows(nx, ny, nz, f, m),
+           "Brick3D": lambda f, m: oe.brick3d_rows(nx, ny, nz, f, m)}[kind]
+    for p in range(P):
+        first, nloc = oe.uniform_map(n_global, P, p)
+        rp, gc, vv = gen(first, nloc)
+        plan = lib_plan(n_global, P, p, rp, gc, vv)
+        xc = xspace_cols(plan, first, nloc)
+        lv = plan["lvals"]
+        rp = np.asarray(rp, dtype=np.int64)
+        res = lib_pair_templates(nloc, rp, xc, lv)
+        assert res is not None
+        tid, rec, dic = res
+        assert rec.shape[0] <= 64 and len(dic) <= 4
+        seq = replay_pair_templates(nloc, tid, rec, dic)
+        for q in range(len(tid)):
+            rows = range(2 * q, min(nloc, 2 * q + 2))
+            ghost = any((xc[rp[r]:rp[r + 1]] >= nloc).any() for r in rows)
+            assert (tid[q] == 255) == ghost, q
+            if ghost:
+                continue
+            for r in rows:
+                want = list(zip(lv[rp[r]:rp[r + 1]].tolist(), xc[rp[r]:rp[r + 1]].tolist()))
+                got = [(float(v), c) for v, c in seq[r]]
+                assert len(got) == len(want) and all(
+                    np.float64(a).tobytes() == np.float64(b).tobytes() and c == d
+                    for (a, c), (b, d) in zip(got, want)), r
+
+
+def test_pair_templates_reject_unstructured():
+    """Random rows do not repeat shapes: no template plan (the operator keeps its pair / SELL
+    kernel); repeated columns are refused; an odd row count leaves a one-row last pair."""
+    n = 2001
+    rp, gc, vv = random_rows(n, 0, n, 3, per_row=6)
+    plan = lib_plan(n, 1, 0, rp, gc, vv)
+    xc = xspace_cols(plan, 0, n)
+    assert lib_pair_templates(n, np.asarray(rp, dtype=np.int64), xc, plan["lvals"]) is None
+    rp = np.array([0, 2, 3])
+    assert lib_pair_templates(2, rp, np.array([1, 1, 0], dtype=np.int32), np.ones(3)) is None
+    rp = np.array([0, 2, 3, 5])
+    xc = np.array([0, 2, 1, 0, 2], dtype=np.int32)
+    tid, rec, dic = lib_pair_templates(3, rp, xc, np.array([1.0, 2.0, 3.0, 1.0, 2.0]))
+    seq = replay_pair_templates(3, tid, rec, dic)
+    assert seq == [[(1.0, 0), (2.0, 2)], [(3.0, 1)], [(1.0, 0), (2.0, 2)]]

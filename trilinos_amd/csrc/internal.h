@@ -80,6 +80,10 @@ void launch_spmm_sell(hipStream_t s, int n_local, const long long *off, const in
 void launch_spmm(hipStream_t s, int row_begin, int row_end, const int *rowptr, const int *cols,
                  const double *vals, MvDesc X, int n_local, const double *ghost, long long ldg,
                  MvDesc Y, double alpha, double beta, const int *sel = nullptr, int nsel = 0);
+// Row-pair templates (make_pair_templates): every pair whose template id is not kTplNone;
+// the others are left to one of the kernels above.
+void launch_spmm_tpl(hipStream_t s, int n_local, const unsigned char *tid, const int2 *rec, int ntpl, int maxk,
+                     const double *vals, int nvals, MvDesc X, MvDesc Y, double alpha, double beta);
 
 // Partial products for C = A^T B over `nrows` rows: writes nblocks x (L*kb) partials.
 int gemm_tn_blocks(int nrows);

@@ -381,6 +381,242 @@ void launch_spmm_pair(hipStream_t s, int n_local, int max_keys, int rmax, const 
 }
 
 // -------------------------------------------------------------------------------------
+// SpMM x k over row-pair TEMPLATES (plan: make_pair_templates, plan.cpp).  Same arithmetic
+// as k_spmm_pair -- one thread per row pair, 16-byte loads of aligned X row pairs, each
+// row's products added in stored order, no FMA -- but the matrix is read as one template
+// byte per pair: the template's keys (offsets from the pair) and coefficient slots sit in
+// LDS, the coefficients in a value dictionary (slot 255 = no entry, value 0, never added).
+// For a stencil operator this removes the 12 bytes per entry of the CSR stream, leaving X
+// (gathered, mostly from L2) and Y.  Pairs marked kTplNone (they read ghost columns) are
+// skipped here and computed by the fallback kernel.  Grid-stride over resident workgroups,
+// so the LDS tables are loaded once per workgroup.  Per key the next key's KC loads are
+// issued before the current key's products (two keys' loads in flight).
+// -------------------------------------------------------------------------------------
+template <int KC>
+__global__ __launch_bounds__(256) void k_spmm_tpl(int npairs, int n_local, const unsigned char *__restrict__ tid,
+                                                  const int2 *__restrict__ rec, int maxk, int nrec,
+                                                  const double *__restrict__ vals, int nvals, MvDesc X, MvDesc Y,
+                                                  int c0, int kc, double alpha, double beta) {
+#pragma clang fp contract(off)
+  extern __shared__ double tpl_lds[];
+  double *s_val = tpl_lds;                   // 256 dictionary slots (255: none, 0.0)
+  int2 *s_rec = (int2 *)(tpl_lds + 256);     // ntpl * maxk key records
+  s_val[threadIdx.x] = (int)threadIdx.x < nvals ? vals[threadIdx.x] : 0.0;
+  for (int i = threadIdx.x; i < nrec; i += 256) s_rec[i] = rec[i];
+  __syncthreads();
+  const double *xc[KC];
+  double *yc[KC];
+#pragma unroll
+  for (int c = 0; c < KC; ++c) {
+    xc[c] = colp(X, c0 + (c < kc ? c : 0));
+    yc[c] = colp(Y, c0 + (c < kc ? c : 0));
+  }
+  for (int p = blockIdx.x * 256 + threadIdx.x; p < npairs; p += gridDim.x * 256) {
+    const int t = tid[p];
+    if (t == 0xFF) continue;
+    const int2 *r = s_rec + t * maxk;
+    double sa[KC], sb[KC];
+#pragma unroll
+    for (int c = 0; c < KC; ++c) sa[c] = sb[c] = 0.0;
+    d2 xn[KC];
+    int2 qn = r[0];
+#pragma unroll
+    for (int c = 0; c < KC; ++c) xn[c] = *(const d2 *)(xc[c] + 2LL * (p + qn.x));
+    for (int u = 0; u < maxk; ++u) {
+      d2 x[KC];
+#pragma unroll
+      for (int c = 0; c < KC; ++c) x[c] = xn[c];
+      const unsigned sl = (unsigned)qn.y;
+      if (u + 1 < maxk) {  // uniform: issue the next key's loads before these products
+        qn = r[u + 1];
+#pragma unroll
+        for (int c = 0; c < KC; ++c) xn[c] = *(const d2 *)(xc[c] + 2LL * (p + qn.x));
+      }
+      const unsigned s0 = sl & 0xFF, s1 = (sl >> 8) & 0xFF, s2 = (sl >> 16) & 0xFF, s3 = sl >> 24;
+      const double v0 = s_val[s0], v1 = s_val[s1], v2 = s_val[s2], v3 = s_val[s3];
+#pragma unroll
+      for (int c = 0; c < KC; ++c) {
+        const double pa0 = v0 * x[c].x, pa1 = v1 * x[c].y;
+        const double pb0 = v2 * x[c].x, pb1 = v3 * x[c].y;
+        sa[c] = sa[c] + (s0 != 0xFF ? pa0 : 0.0);
+        sa[c] = sa[c] + (s1 != 0xFF ? pa1 : 0.0);
+        sb[c] = sb[c] + (s2 != 0xFF ? pb0 : 0.0);
+        sb[c] = sb[c] + (s3 != 0xFF ? pb1 : 0.0);
+      }
+    }
+    const int ra = 2 * p;
+    const bool hasb = ra + 1 < n_local;
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+      if (c >= kc) break;
+      double *yp = yc[c] + ra;
+      double a = sa[c], b = sb[c];
+      if (beta == 0.0) {
+        if (alpha != 1.0) {
+          a = alpha * a;
+          b = alpha * b;
+        }
+      } else {
+        a = alpha * a + beta * yp[0];
+        if (hasb) b = alpha * b + beta * yp[1];
+      }
+      if (hasb)
+        *(d2 *)yp = d2{a, b};
+      else
+        yp[0] = a;
+    }
+  }
+}
+
+// Short templates (at most 12 keys per pair: 5- and 7-point stencils): the pair's key
+// offsets and coefficients are taken into registers once, then the KC columns are swept
+// with all of a column's MAXK loads in flight (the k_spmm_pair loop without its plan
+// stream).  Instantiated for the exact key count.
+template <int KC, int MAXK>
+__global__ __launch_bounds__(256) void k_spmm_tplr(int npairs, int n_local, const unsigned char *__restrict__ tid,
+                                                   const int2 *__restrict__ rec, int nrec,
+                                                   const double *__restrict__ vals, int nvals, MvDesc X, MvDesc Y,
+                                                   int c0, int kc, double alpha, double beta) {
+#pragma clang fp contract(off)
+  extern __shared__ double tpl_lds[];
+  double *s_val = tpl_lds;
+  int2 *s_rec = (int2 *)(tpl_lds + 256);
+  s_val[threadIdx.x] = (int)threadIdx.x < nvals ? vals[threadIdx.x] : 0.0;
+  for (int i = threadIdx.x; i < nrec; i += 256) s_rec[i] = rec[i];
+  __syncthreads();
+  for (int p = blockIdx.x * 256 + threadIdx.x; p < npairs; p += gridDim.x * 256) {
+    const int t = tid[p];
+    if (t == 0xFF) continue;
+    int key[MAXK];
+    double cx[MAXK][4];
+    unsigned long long use = 0;
+#pragma unroll
+    for (int u = 0; u < MAXK; ++u) {
+      const int2 q = s_rec[t * MAXK + u];
+      key[u] = p + q.x;
+#pragma unroll
+      for (int sl = 0; sl < 4; ++sl) {
+        const unsigned s = ((unsigned)q.y >> (8 * sl)) & 0xFF;
+        cx[u][sl] = s_val[s];
+        use |= (s != 0xFF ? 1ull : 0ull) << (4 * u + sl);
+      }
+    }
+    const int ra = 2 * p;
+    const bool hasb = ra + 1 < n_local;
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+      if (c >= kc) break;
+      const double *xc = colp(X, c0 + c);
+      d2 x[MAXK];
+#pragma unroll
+      for (int u = 0; u < MAXK; ++u) x[u] = *(const d2 *)(xc + 2LL * key[u]);
+      double sa = 0.0, sb = 0.0;
+#pragma unroll
+      for (int u = 0; u < MAXK; ++u) {
+        const double pa0 = cx[u][0] * x[u].x, pa1 = cx[u][1] * x[u].y;
+        const double pb0 = cx[u][2] * x[u].x, pb1 = cx[u][3] * x[u].y;
+        sa = sa + ((use >> (4 * u)) & 1ull ? pa0 : 0.0);
+        sa = sa + ((use >> (4 * u + 1)) & 1ull ? pa1 : 0.0);
+        sb = sb + ((use >> (4 * u + 2)) & 1ull ? pb0 : 0.0);
+        sb = sb + ((use >> (4 * u + 3)) & 1ull ? pb1 : 0.0);
+      }
+      double *yp = colp(Y, c0 + c) + ra;
+      if (beta == 0.0) {
+        if (alpha != 1.0) {
+          sa = alpha * sa;
+          sb = alpha * sb;
+        }
+      } else {
+        sa = alpha * sa + beta * yp[0];
+        if (hasb) sb = alpha * sb + beta * yp[1];
+      }
+      if (hasb)
+        *(d2 *)yp = d2{sa, sb};
+      else
+        yp[0] = sa;
+    }
+  }
+}
+
+static int tpl_resident_blocks(const void *kern, size_t lds) {
+  int dev = 0, ncu = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+    ncu = 256;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, lds) != hipSuccess || per_cu < 1)
+    per_cu = 1;
+  return ncu * per_cu;
+}
+
+template <class K>
+static void tpl_launch(K kern, hipStream_t s, size_t lds, int npairs, const void *key) {
+  // resident grid per (kernel, table size): grid-stride loops load the LDS tables once per
+  // workgroup
+  static thread_local std::vector<std::pair<std::pair<const void *, size_t>, int>> cache;
+  int resident = 0;
+  for (auto &e : cache)
+    if (e.first.first == key && e.first.second == lds) resident = e.second;
+  if (!resident) {
+    resident = tpl_resident_blocks(key, lds);
+    cache.push_back({{key, lds}, resident});
+  }
+  kern(std::min(cdiv(npairs, 256), resident));
+}
+
+template <int KC>
+static void tpl_cols(hipStream_t s, size_t lds, int npairs, int n_local, const unsigned char *tid, const int2 *rec,
+                     int maxk, int nrec, const double *vals, int nvals, MvDesc X, MvDesc Y, int c0, int kc,
+                     double alpha, double beta) {
+#define TPLR_CASE(K)                                                                                          \
+  case K:                                                                                                     \
+    tpl_launch([&](int grid) { k_spmm_tplr<KC, K><<<grid, 256, lds, s>>>(npairs, n_local, tid, rec, nrec, vals, \
+                                                                        nvals, X, Y, c0, kc, alpha, beta); }, \
+               s, lds, npairs, (const void *)k_spmm_tplr<KC, K>);                                             \
+    return;
+  switch (maxk) {
+    TPLR_CASE(1)
+    TPLR_CASE(2)
+    TPLR_CASE(3)
+    TPLR_CASE(4)
+    TPLR_CASE(5)
+    TPLR_CASE(6)
+    TPLR_CASE(7)
+    TPLR_CASE(8)
+    TPLR_CASE(9)
+    TPLR_CASE(10)
+    TPLR_CASE(11)
+    TPLR_CASE(12)
+    default:
+      break;
+  }
+#undef TPLR_CASE
+  tpl_launch([&](int grid) { k_spmm_tpl<KC><<<grid, 256, lds, s>>>(npairs, n_local, tid, rec, maxk, nrec, vals, nvals,
+                                                                  X, Y, c0, kc, alpha, beta); },
+             s, lds, npairs, (const void *)k_spmm_tpl<KC>);
+}
+
+void launch_spmm_tpl(hipStream_t s, int n_local, const unsigned char *tid, const int2 *rec, int ntpl, int maxk,
+                     const double *vals, int nvals, MvDesc X, MvDesc Y, double alpha, double beta) {
+  const int npairs = (n_local + 1) / 2;
+  if (npairs <= 0) return;
+  const int nrec = ntpl * maxk;
+  const size_t lds = sizeof(double) * 256 + sizeof(int2) * (size_t)nrec;
+  const int k = Y.ncols;
+  for (int c0 = 0; c0 < k; c0 += 8) {
+    const int kc = (k - c0) < 8 ? (k - c0) : 8;
+    if (kc == 1)
+      tpl_cols<1>(s, lds, npairs, n_local, tid, rec, maxk, nrec, vals, nvals, X, Y, c0, kc, alpha, beta);
+    else if (kc <= 2)
+      tpl_cols<2>(s, lds, npairs, n_local, tid, rec, maxk, nrec, vals, nvals, X, Y, c0, kc, alpha, beta);
+    else if (kc <= 4)
+      tpl_cols<4>(s, lds, npairs, n_local, tid, rec, maxk, nrec, vals, nvals, X, Y, c0, kc, alpha, beta);
+    else
+      tpl_cols<8>(s, lds, npairs, n_local, tid, rec, maxk, nrec, vals, nvals, X, Y, c0, kc, alpha, beta);
+    LAUNCH_CHECK();
+  }
+}
+
+// -------------------------------------------------------------------------------------
 // C = A^T B (A: nrows x L, B: nrows x kb <= 16) on v_mfma_f64_16x16x4_f64.
 // MFMA M = 16 columns of A (one column tile), N = 16 columns of B, K = rows.
 // The K index of an MFMA may map to ANY row as long as A and B agree, so each lane loads

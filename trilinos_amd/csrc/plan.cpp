@@ -3,6 +3,7 @@
 #include "plan.h"
 
 #include <algorithm>
+#include <climits>
 #include <cstring>
 #include <numeric>
 #include <unordered_map>
@@ -371,6 +372,121 @@ void make_pair_sell(int n_local, const long long *rowptr, const double *lvals, c
       }
     }
   }
+}
+
+bool make_pair_templates(int n_local, const long long *rowptr, const int *xcols, const double *lvals,
+                         PairTemplates &out) {
+  const int P = (n_local + 1) / 2;
+  out = PairTemplates();
+  out.npairs = P;
+  out.id.assign((size_t)P, kTplNone);
+  std::unordered_map<unsigned long long, int> val_index;  // value bit pattern -> dictionary slot
+  // a pair's shape: key count, then per key (offset, packed slots); templates are found by
+  // comparing against the previous pair's shape first (runs of interior pairs) and then by
+  // a hash of the shape
+  std::vector<long long> shape, prev;
+  int prev_id = -1;
+  std::unordered_map<std::string, int> tpl_index;
+  std::vector<std::vector<long long>> shapes;
+  auto value_slot = [&](double v, int *slot) {
+    unsigned long long bits;
+    std::memcpy(&bits, &v, sizeof(bits));
+    if (out.vals.size() <= 8) {  // stencils: a handful of values, a linear scan beats hashing
+      for (size_t i = 0; i < out.vals.size(); ++i)
+        if (std::memcmp(&out.vals[i], &bits, sizeof(bits)) == 0) {
+          *slot = (int)i;
+          return true;
+        }
+    }
+    auto it = val_index.find(bits);
+    if (it != val_index.end()) {
+      *slot = it->second;
+      return true;
+    }
+    if (out.vals.size() >= 255) return false;
+    *slot = (int)out.vals.size();
+    val_index.emplace(bits, *slot);
+    out.vals.push_back(v);
+    return true;
+  };
+  for (int p = 0; p < P; ++p) {
+    long long b[2], e[2];
+    bool ghost = false;
+    for (int h = 0; h < 2; ++h) {
+      const int r = 2 * p + h;
+      b[h] = r < n_local ? rowptr[r] : 0;
+      e[h] = r < n_local ? rowptr[r + 1] : 0;
+      if (e[h] - b[h] > kTplMaxRow) return false;
+      for (long long i = b[h]; i < e[h]; ++i) {
+        if (xcols[i] >= n_local) ghost = true;
+        if (i > b[h] && xcols[i] <= xcols[i - 1]) return false;  // stored order must ascend
+      }
+    }
+    if (ghost) continue;
+    // merge the two rows' keys in ascending order (both rows ascend, so key order is each
+    // row's stored order, low half before high half)
+    shape.clear();
+    shape.push_back(0);
+    long long i0 = b[0], i1 = b[1];
+    int nk = 0;
+    while (i0 < e[0] || i1 < e[1]) {
+      const int k0 = i0 < e[0] ? (xcols[i0] >> 1) : INT32_MAX;
+      const int k1 = i1 < e[1] ? (xcols[i1] >> 1) : INT32_MAX;
+      const int key = k0 < k1 ? k0 : k1;
+      unsigned slots = 0xFFFFFFFFu;
+      long long *it[2] = {&i0, &i1};
+      for (int h = 0; h < 2; ++h)
+        while (*it[h] < e[h] && (xcols[*it[h]] >> 1) == key) {
+          const int sh = 8 * (2 * h + (xcols[*it[h]] & 1));
+          int vs;
+          if (!value_slot(lvals[*it[h]], &vs)) return false;
+          slots = (slots & ~(0xFFu << sh)) | ((unsigned)vs << sh);
+          ++*it[h];
+        }
+      shape.push_back(key - p);
+      shape.push_back((long long)slots);
+      if (++nk > kTplMaxKeys) return false;
+    }
+    shape[0] = nk;
+    int t;
+    if (prev_id >= 0 && shape == prev) {
+      t = prev_id;
+    } else {
+      std::string s((const char *)shape.data(), sizeof(long long) * shape.size());
+      auto it = tpl_index.find(s);
+      if (it != tpl_index.end()) {
+        t = it->second;
+      } else {
+        if ((int)shapes.size() >= kTplMaxTemplates) return false;
+        t = (int)shapes.size();
+        tpl_index.emplace(std::move(s), t);
+        shapes.push_back(shape);
+      }
+      prev = shape;
+      prev_id = t;
+    }
+    out.id[(size_t)p] = (unsigned char)t;
+    ++out.n_templated;
+    out.maxk = std::max(out.maxk, nk);
+  }
+  if (out.n_templated == 0) return false;
+  out.ntpl = (int)shapes.size();
+  out.maxk = std::max(out.maxk, 1);
+  out.rec.assign((size_t)out.ntpl * out.maxk * 2, 0);
+  for (int t = 0; t < out.ntpl; ++t) {
+    const auto &sh = shapes[(size_t)t];
+    for (int u = 0; u < out.maxk; ++u) {
+      int *r = &out.rec[((size_t)t * out.maxk + u) * 2];
+      if (u < sh[0]) {
+        r[0] = (int)sh[(size_t)(1 + 2 * u)];
+        r[1] = (int)(unsigned)sh[(size_t)(2 + 2 * u)];
+      } else {
+        r[0] = 0;  // padding key: reads the pair itself, adds nothing
+        r[1] = (int)0xFFFFFFFFu;
+      }
+    }
+  }
+  return true;
 }
 
 void make_sell64(int n_local, const long long *rowptr, const int *lcols, const double *lvals, Sell64 &out) {

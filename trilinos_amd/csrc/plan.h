@@ -70,6 +70,35 @@ struct Sell64 {
 };
 void make_sell64(int n_local, const long long *rowptr, const int *lcols, const double *lvals, Sell64 &out);
 
+// Row-pair templates for k_spmm_tpl (kernels.hip): a compressed form of the pair plan for
+// matrices whose row pairs repeat a small number of shapes (stencils: the interior pairs of
+// a 7- or 27-point operator are all alike, boundary pairs add a few dozen variants).  A
+// pair's template is its keys relative to the pair index (owned columns only), and per key
+// which entry of which row reads the low / high half, with the coefficient stored as an
+// index into a value dictionary.  Per pair the matrix then costs ONE byte (its template id)
+// instead of 12 bytes per entry; the sums still run in stored order with the same products,
+// so the result is bit-identical to k_spmm / k_spmm_pair.
+//   id[p]                   template of pair p (kTplNone: the pair reads a ghost column and
+//                           is left to the fallback kernel)
+//   rec[(t * maxk + u)]     key u of template t: .x = key offset (X rows 2 (p + off), +1),
+//                           .y = four value-dictionary slots (bytes: row 0 low, row 0 high,
+//                           row 1 low, row 1 high; kTplUnused = no entry); templates with
+//                           fewer keys are padded with (0, all unused)
+//   vals[i]                 the value dictionary (distinct coefficients, bit patterns)
+// Returns false (format not used) when a row has more than kTplMaxRow entries, a pair more
+// than kTplMaxKeys keys, there are more than kTplMaxTemplates templates or more than 255
+// distinct values, a row repeats a column, or no pair is templated.
+constexpr int kTplMaxRow = 32, kTplMaxKeys = 32, kTplMaxTemplates = 128;
+constexpr unsigned char kTplNone = 0xFF, kTplUnused = 0xFF;
+struct PairTemplates {
+  int ntpl = 0, maxk = 0, npairs = 0, n_templated = 0;
+  std::vector<unsigned char> id;
+  std::vector<int> rec;  // 2 ints per key: offset, packed slots
+  std::vector<double> vals;
+};
+bool make_pair_templates(int n_local, const long long *rowptr, const int *xcols, const double *lvals,
+                         PairTemplates &out);
+
 void galeri_rows(const std::string &kind, int nx, int ny, int nz, long long first, int n_local,
                  std::vector<long long> &rowptr, std::vector<long long> &gcols,
                  std::vector<double> &vals);

@@ -654,7 +654,8 @@ void mv_assign(const migmres_mv &A, migmres_mv &Y) {
 // distributed CRS operator
 // ------------------------------------------------------------------------------------
 migmres_crs::~migmres_crs() {
-  for (void *p : {(void *)d_soff, (void *)d_slen, (void *)d_scol, (void *)d_sval})
+  for (void *p : {(void *)d_soff, (void *)d_slen, (void *)d_scol, (void *)d_sval, (void *)d_tpl_id,
+                  (void *)d_tpl_rec, (void *)d_tpl_val, (void *)d_tpl_rest})
     if (p) hipFree(p);
   for (void *p : {(void *)d_export_grp, (void *)d_remote_grp, (void *)d_recv})
     if (p) hipFree(p);
@@ -798,6 +799,42 @@ migmres_crs *crs_create(migmres_ctx *ctx, long long n_global, long long first, i
         A->use_sell = true;
       }
     }
+    A->spmm_fixed_bytes = 12.0 * nnz + 4.0 * (n_local + 1);
+    {
+      // row-pair templates: the pairs' shapes repeat (stencils) -> one byte per pair
+      const char *nt = std::getenv("MIGMRES_NO_TPL_SPMM");
+      PairTemplates pt;
+      if (!(nt && nt[0] == '1') && n_local > 0 &&
+          make_pair_templates(n_local, rowptr, lcols.data(), lvals.data(), pt)) {
+        std::vector<int> rest;
+        double rest_bytes = 0.0;
+        for (int q = 0; q < pt.npairs; ++q) {
+          if (pt.id[(size_t)q] != kTplNone) continue;
+          if (A->use_pairs) rest.push_back(q);
+          for (int r = 2 * q; r < std::min(n_local, 2 * q + 2); ++r) {
+            if (!A->use_pairs) rest.push_back(r);
+            rest_bytes += 12.0 * (double)(rowptr[r + 1] - rowptr[r]) + 4.0;
+          }
+        }
+        MIG_HIP(hipMalloc(&A->d_tpl_id, pt.id.size()));
+        MIG_HIP(hipMalloc(&A->d_tpl_rec, sizeof(int) * pt.rec.size()));
+        MIG_HIP(hipMalloc(&A->d_tpl_val, sizeof(double) * (pt.vals.size() + 1)));
+        MIG_HIP(hipMemcpy(A->d_tpl_id, pt.id.data(), pt.id.size(), hipMemcpyHostToDevice));
+        MIG_HIP(hipMemcpy(A->d_tpl_rec, pt.rec.data(), sizeof(int) * pt.rec.size(), hipMemcpyHostToDevice));
+        if (!pt.vals.empty())
+          MIG_HIP(hipMemcpy(A->d_tpl_val, pt.vals.data(), sizeof(double) * pt.vals.size(), hipMemcpyHostToDevice));
+        if (!rest.empty()) {
+          MIG_HIP(hipMalloc(&A->d_tpl_rest, sizeof(int) * rest.size()));
+          MIG_HIP(hipMemcpy(A->d_tpl_rest, rest.data(), sizeof(int) * rest.size(), hipMemcpyHostToDevice));
+        }
+        A->n_tpl_rest = (int)rest.size();
+        A->tpl_ntpl = pt.ntpl;
+        A->tpl_maxk = pt.maxk;
+        A->tpl_nvals = (int)pt.vals.size();
+        A->use_tpl = true;
+        A->spmm_fixed_bytes = (double)pt.npairs + 8.0 * pt.rec.size() / 2 + 8.0 * pt.vals.size() + rest_bytes;
+      }
+    }
     if (n_remote > 0) {
       // interior / boundary units for the halo overlap (a unit is a row pair with the
       // row-pair kernel, else a row; boundary = reads at least one ghost column)
@@ -898,8 +935,15 @@ void crs_apply(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, double alpha,
     MIG_HIP(hipEventRecord(c->ev_halo, c->halo_stream));
     c->comm_seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
-  ProfScope ps(c, K_SPMM, 12.0 * A.nnz + 4.0 * (A.n_local + 1) + 8.0 * A.n_local * k * (beta == 0.0 ? 2.0 : 3.0));
-  if (halo && A.d_sel_int) {
+  ProfScope ps(c, K_SPMM, A.spmm_fixed_bytes + 8.0 * A.n_local * k * (beta == 0.0 ? 2.0 : 3.0));
+  if (A.use_tpl) {
+    // templated pairs read no ghost column: they run while the halo is in flight, then the
+    // pairs that do read one go to the fallback kernel
+    launch_spmm_tpl(c->stream, A.n_local, A.d_tpl_id, A.d_tpl_rec, A.tpl_ntpl, A.tpl_maxk, A.d_tpl_val,
+                    A.tpl_nvals, X.desc(), Y.desc(), alpha, beta);
+    if (halo) MIG_HIP(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
+    if (A.n_tpl_rest > 0) spmm(A.d_tpl_rest, A.n_tpl_rest);
+  } else if (halo && A.d_sel_int) {
     // interior rows while the halo is in flight, then the rows that read ghost columns
     spmm(A.d_sel_int, A.n_sel_int);
     MIG_HIP(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
@@ -918,7 +962,10 @@ void crs_apply(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, double alpha,
 extern "C" int migmres_crs_spmm_kernel(const migmres_crs *A, int *kind) {
   return guard([&] {
     MIG_CHECK(A && kind, "bad arguments");
-    *kind = A->use_pairs ? MIGMRES_SPMM_PAIR : A->use_sell ? MIGMRES_SPMM_SELL : MIGMRES_SPMM_CSR;
+    *kind = A->use_tpl ? MIGMRES_SPMM_TPL
+            : A->use_pairs ? MIGMRES_SPMM_PAIR
+            : A->use_sell  ? MIGMRES_SPMM_SELL
+                           : MIGMRES_SPMM_CSR;
   });
 }
 extern "C" int migmres_map_uniform(long long n_global, int nranks, int rank, long long *first,
@@ -975,6 +1022,23 @@ extern "C" int migmres_plan_pairs(int n_local, const long long *rowptr, const in
     if (ptr_out) std::memcpy(ptr_out, pp.ptr.data(), sizeof(int) * pp.ptr.size());
     if (key_out) std::memcpy(key_out, pp.key.data(), sizeof(int) * pp.key.size());
     if (meta_out) std::memcpy(meta_out, pp.meta.data(), sizeof(unsigned short) * pp.meta.size());
+  });
+}
+
+extern "C" int migmres_plan_pair_templates(int n_local, const long long *rowptr, const int *xcols, const double *vals,
+                                           unsigned char *id_out, int *rec_out, double *vals_out, int *ntpl,
+                                           int *maxk, int *nvals, int *ok) {
+  return guard([&] {
+    MIG_CHECK(n_local >= 0 && rowptr && ntpl && maxk && nvals && ok, "plan_pair_templates: bad arguments");
+    PairTemplates pt;
+    *ok = make_pair_templates(n_local, rowptr, xcols, vals, pt) ? 1 : 0;
+    *ntpl = *ok ? pt.ntpl : 0;
+    *maxk = *ok ? pt.maxk : 0;
+    *nvals = *ok ? (int)pt.vals.size() : 0;
+    if (!*ok) return;
+    if (id_out) std::memcpy(id_out, pt.id.data(), pt.id.size());
+    if (rec_out) std::memcpy(rec_out, pt.rec.data(), sizeof(int) * pt.rec.size());
+    if (vals_out) std::memcpy(vals_out, pt.vals.data(), sizeof(double) * pt.vals.size());
   });
 }
 

@@ -144,6 +144,18 @@ struct migmres_crs {
   int *d_slen = nullptr, *d_scol = nullptr;
   double *d_sval = nullptr;
   bool use_sell = false;
+  // row-pair templates (k_spmm_tpl) when the pairs repeat a few shapes: templated pairs run
+  // there (reading no ghost column, they also make the interior half of the halo overlap);
+  // the rest -- pairs that read a ghost column -- go to the kernel above through
+  // d_tpl_rest (its units: pairs for the pair kernel, rows otherwise)
+  unsigned char *d_tpl_id = nullptr;
+  int2 *d_tpl_rec = nullptr;
+  double *d_tpl_val = nullptr;
+  int tpl_ntpl = 0, tpl_maxk = 0, tpl_nvals = 0;
+  bool use_tpl = false;
+  int *d_tpl_rest = nullptr;
+  int n_tpl_rest = 0;
+  double spmm_fixed_bytes = 0.0;  // matrix-format bytes one apply reads (bench accounting)
   // interior / boundary split (units = pairs with the row-pair kernel, else rows): interior
   // units read no ghost column and run while the halo exchange is in flight
   int *d_sel_int = nullptr, *d_sel_bnd = nullptr;
