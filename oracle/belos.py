@@ -82,6 +82,35 @@ def _coldots(X, Y):
     return np.einsum("ij,ij->j", X, Y)
 
 
+# MultiVecTraits operations on host arrays (rows x columns), as the Epetra adapter maps them
+# (belos/epetra/src/BelosEpetraAdapter.hpp: MvTimesMatAddMv -> Epetra_MultiVector::Multiply('N',
+# 'N'), MvTransMv -> Multiply('T','N'), MvDot -> Dot, MvNorm -> Norm1/Norm2/NormInf;
+# epetra/src/Epetra_MultiVector.cpp:1936-2083, 1123-1156, 1547-1577).  The ICGS restatement
+# below uses the same products (_tn, Q @ C, _coldots); these are what
+# tests/test_oracle_pins.py pins to Epetra's own MultiVector known answers.
+def mv_times_mat_add_mv(alpha, A, B, beta, C):
+    """C <- alpha A B + beta C  (Multiply('N','N', alpha, A, B, beta))."""
+    return alpha * (A @ B) + beta * C
+
+
+def mv_trans_mv(alpha, A, B, beta=0.0, C=None):
+    """alpha A^T B + beta C  (Multiply('T','N', alpha, A, B, beta))."""
+    out = alpha * _tn(A, B)
+    return out if C is None else out + beta * C
+
+
+def mv_dot(A, B):
+    return _coldots(A, B)
+
+
+def mv_norm(A, kind="2"):
+    if kind == "1":
+        return np.abs(A).sum(axis=0)
+    if kind == "inf":
+        return np.abs(A).max(axis=0)
+    return np.sqrt(_coldots(A, A))
+
+
 # ---------------------------------------------------------------------------
 # ICGS
 # ---------------------------------------------------------------------------

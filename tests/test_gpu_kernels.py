@@ -252,3 +252,38 @@ def test_dgks_project_normalize(comm, k, near_dep):
     np.testing.assert_allclose(C, Co, rtol=1e-10, atol=1e-12)
     np.testing.assert_allclose(B, Bo, rtol=1e-10, atol=1e-12)
     np.testing.assert_allclose(Xd.download(), Xo, rtol=1e-9, atol=1e-11)
+
+
+@pytest.mark.parametrize("n", [10, 4099, 100003])
+def test_epetra_gemm_known_answers(comm, n):
+    """Epetra's own MultiVector GEMM known answers (BuildTestProblems.cpp:45-268 via
+    ExecuteTestProblems.cpp:155-215) through the C ABI: MvTransMv (case 2, alpha 2, beta 1 on
+    the host side as Belos applies it) and MvTimesMatAddMv (cases 6-7, alpha 2, beta 1.1),
+    under the reference's BadResidual threshold and a 1e-13 relative bar; plus the LocalMap
+    Norm1 / Dot / Norm2 closed forms (ExecuteTestProblems.cpp:227-272)."""
+    import trilinos_amd as ta
+    from tests.test_oracle_pins import epetra_gemm_kat, BAD_RESIDUAL
+    MVT = ta.MultiVecTraits
+    nv = 4
+    A, B, C0, want = epetra_gemm_kat(2, n, nv, 2.0, 1.0)
+    got = MVT.MvTransMv(2.0, _upload(ta, comm, A), _upload(ta, comm, B)) + 1.0 * C0
+    assert np.linalg.norm(got - want, axis=0).max() <= BAD_RESIDUAL
+    np.testing.assert_allclose(got, want, rtol=1e-13)
+    A, B, C0, want = epetra_gemm_kat(3, n, nv, 2.0, 1.1)
+    Cd = _upload(ta, comm, C0)
+    MVT.MvTimesMatAddMv(2.0, _upload(ta, comm, A), B, 1.1, Cd)
+    got = Cd.download()
+    assert np.linalg.norm(got - want, axis=0).max() <= BAD_RESIDUAL
+    np.testing.assert_allclose(got, want, rtol=1e-13)
+    L = 10
+    A = np.zeros((L, nv))
+    for j in range(nv):
+        A[:L - 1, j] = np.arange(1, L)
+        A[L - 1, j] = L + j
+    dl = float(L)
+    norm1 = (dl - 1.0) * dl / 2.0 + A[L - 1]
+    dot = (dl - 1.0) * dl * (2.0 * (dl - 1.0) + 1.0) / 6.0 + A[L - 1] * A[L - 1]
+    Ad = _upload(ta, comm, A)
+    assert np.array_equal(MVT.MvNorm(Ad, ta.OneNorm), norm1)
+    assert np.array_equal(MVT.MvDot(Ad, Ad), dot)
+    np.testing.assert_allclose(MVT.MvNorm(Ad), np.sqrt(dot), rtol=1e-15)

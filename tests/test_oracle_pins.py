@@ -51,6 +51,72 @@ def test_epetra_multivector_closed_forms():
     np.testing.assert_allclose(np.linalg.norm(A, axis=0), np.sqrt(dot), rtol=1e-15)
 
 
+def epetra_gemm_kat(case, n, nv, alpha, beta, transb="N", seed=3):
+    """Epetra's GEMM known answers (epetra/test/MultiVector/BuildTestProblems.cpp:45-268, driven
+    by ExecuteTestProblems.cpp:155-215): returns A, B, C0 and the closed-form result C_GEMM.
+    case 2: A, B distributed (n x nv), C local (nv x nv): C = alpha A^T B + beta C0,
+            A(i,j) = ((i+1)/n)(j+1), B(i,j) = 1/(((i+1)/n)(j+1)), C_GEMM(i,j) = alpha (i+1) n/(j+1) + beta C0
+    case 3: A distributed (n x nv), B local (nv x nv, transposed when transb = "T"), C distributed:
+            C = alpha A op(B) + beta C0, A(i,j) = ((i+1)/nv)(j+1), B(i,j) = 1/(((i+1)/nv)(j+1)),
+            C_GEMM(i,j) = alpha (i+1) nv/(j+1) + beta C0."""
+    rng = np.random.default_rng(seed)
+    sf = float(n if case == 2 else nv)
+    fi = np.arange(1, n + 1, dtype=float)[:, None]
+    fj = np.arange(1, nv + 1, dtype=float)[None, :]
+    A = (fi * (1.0 / sf)) * fj
+    if case == 2:
+        B = 1.0 / ((fi * (1.0 / sf)) * fj)
+        C0 = rng.uniform(-1, 1, (nv, nv))
+        gi = np.arange(1, nv + 1, dtype=float)[:, None] * sf
+    else:
+        bi = np.arange(1, nv + 1, dtype=float)[:, None]
+        B = 1.0 / ((bi * (1.0 / sf)) * fj)
+        if transb == "T":
+            B = B.T.copy()  # op(B) = B^T must equal the case-3 B above
+        C0 = rng.uniform(-1, 1, (n, nv))
+        gi = fi * sf
+    return A, B, C0, alpha * (gi / fj) + beta * C0
+
+
+BAD_RESIDUAL = 5.0e-6  # ExecuteTestProblems.cpp:880-892 (per column 2-norm of C - C_GEMM)
+
+
+@pytest.mark.parametrize("n", [10, 1000, 4099])
+def test_epetra_gemm_known_answers_on_oracle(n):
+    """The oracle's MvTransMv / MvTimesMatAddMv against Epetra's own GEMM known answers:
+    case 2 (2-D dot product via GEMM, alpha 2, beta 1) and cases 6-7 (vector update via GEMM,
+    alpha 2, beta 1.1, B and B^T), under the reference's BadResidual threshold and a 1e-13
+    relative bar."""
+    nv = 4
+    A, B, C0, want = epetra_gemm_kat(2, n, nv, 2.0, 1.0)
+    got = ob.mv_trans_mv(2.0, A, B, 1.0, C0)
+    assert np.linalg.norm(got - want, axis=0).max() <= BAD_RESIDUAL
+    np.testing.assert_allclose(got, want, rtol=1e-13)
+    for tb in ("N", "T"):
+        A, B, C0, want = epetra_gemm_kat(3, n, nv, 2.0, 1.1, tb)
+        got = ob.mv_times_mat_add_mv(2.0, A, B if tb == "N" else B.T, 1.1, C0)
+        assert np.linalg.norm(got - want, axis=0).max() <= BAD_RESIDUAL
+        np.testing.assert_allclose(got, want, rtol=1e-13)
+
+
+def test_epetra_localmap_closed_forms_on_oracle():
+    """ExecuteTestProblems.cpp:227-272 on the oracle's own MvNorm / MvDot: A[j][i] = i+1
+    (i < 9), A[j][9] = 10 + j; Norm1, Dot and Norm2 closed forms (exact in fp64 here)."""
+    L, nv = 10, 4
+    A = np.zeros((L, nv))
+    for j in range(nv):
+        A[:L - 1, j] = np.arange(1, L)
+        A[L - 1, j] = L + j
+    dl = float(L)
+    norm1 = (dl - 1.0) * dl / 2.0 + A[L - 1]
+    dot = (dl - 1.0) * dl * (2.0 * (dl - 1.0) + 1.0) / 6.0 + A[L - 1] * A[L - 1]
+    assert np.array_equal(ob.mv_norm(A, "1"), norm1)
+    assert np.array_equal(ob.mv_dot(A, A), dot)
+    np.testing.assert_allclose(ob.mv_norm(A, "2"), np.sqrt(dot), rtol=1e-15)
+    assert np.abs(ob.mv_norm(A, "2") - np.sqrt(dot)).max() <= BAD_RESIDUAL
+    assert np.array_equal(ob.mv_norm(A, "inf"), A[L - 1])
+
+
 def test_galeri_laplace3d_structure():
     """nnz = 7 m^3 - 6 m^2 (SURVEY.md 8 sizes table); rows sorted by local column."""
     m = 6
