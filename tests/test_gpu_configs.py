@@ -86,6 +86,37 @@ def test_config_solves_match_oracle(comm, case):
     _check(res, ref, Aor, B, res[4], oracle_case_rerun(gen, n, 1, k, params, side, sweeps, damping))
 
 
+@pytest.mark.parametrize("dims,nb,P", [((20, 20, 20), 24, 1), ((18, 17, 16), 23, 2)])
+def test_k16_full_cycle_matches_oracle(comm, dims, nb, P):
+    """Config 3's block size through a whole long cycle (tol 1e-15: never converges, so every
+    block step runs): L = 16 .. 16 (nb - 1), which takes the fused update + projection through
+    both of its k = 16 forms -- all 16 columns in one workgroup (L <= 320) and the column
+    halves in workgroup pairs (L = 336, 352, 368) -- and the Gram-form findBasis at k = 16;
+    counts and residual history against the oracle."""
+    import trilinos_amd as ta
+    k = 16
+    params = _params(k, nb, **{"Convergence Tolerance": 1e-15, "Maximum Iterations": nb, "Maximum Restarts": 0})
+    n, gen = _gen("Laplace3D", dims)
+    Aor, B, ref = _oracle_case(gen, n, P, k, params, None, 0, 0.0)
+    assert not ref["converged"] and ref["iterations"] == nb
+    rerun = oracle_case_rerun(gen, n, P, k, params, None, 0, 0.0)
+    if P == 1:
+        res = _run_case(comm, n, "Laplace3D", dims, k, params, None, 0, 0.0, B)
+        _check(res, ref, Aor, B, res[4], rerun)
+        return
+
+    def rank_fn(c):
+        first = ta.uniform_map(n, c.nranks, c.rank)[0]
+        return first, _run_case(c, n, "Laplace3D", dims, k, params, None, 0, 0.0, B, first)
+
+    out = run_ranks(P, rank_fn)
+    X = np.zeros((n, k))
+    for first, r in out:
+        X[first:first + r[4].shape[0]] = r[4]
+    for first, r in out:
+        _check(r, ref, Aor, B, X, rerun)
+
+
 @pytest.mark.parametrize("case,P", [(0, 2), (0, 4), (2, 2), (5, 3)])
 def test_config_solves_distributed(case, P):
     import trilinos_amd as ta

@@ -64,6 +64,9 @@ void launch_gemm_nn_dot(hipStream_t s, MvDesc A, int L, const double *M, int ldm
 // sink: scratch of nblocks * 256 doubles that absorbs the stores of padding lanes.
 bool nn_tn_supported(int L, int k);
 int nn_tn_blocks(int nrows, int L, int k);
+// k > 8: whether launch_nn_tn runs the column halves in workgroup pairs (partials: half 0
+// [nb/2][L][8] then half 1 [nb/2][L][k-8]) rather than all k columns per workgroup ([nb][L][k]).
+bool nn_tn_paired(int L, int k);
 void launch_nn_tn(hipStream_t s, MvDesc Q, int L, const double *C1, int ldc, MvDesc X, int nrows,
                   double *partial, int nblocks, double *sink, bool store_x1 = true);
 void launch_fb_a(hipStream_t s, MvDesc X, int j, const FbPro &pro, int nrows, double *partial, int nb);

@@ -606,13 +606,13 @@ __global__ __launch_bounds__(16 * RW) void k_nn_tn_w(MvDesc Q, int L, const doub
   // HBM once and the pair's second read hits that XCD's L2 or the Infinity Cache.  Partials:
   // half 0 at [rng][L][8], half 1 after all nrng of them at [rng][L][kx - 8].
   int rng = blockIdx.x, nrng = gridDim.x, h0 = 0;
-  if (kx > 8) {
+  if (kx > 8 && NJ < 4) {
     const int x = blockIdx.x & 15;
     h0 = (x >> 3) * 8;
     rng = (blockIdx.x >> 4) * 8 + (x & 7);
     nrng = gridDim.x >> 1;
   }
-  const int k = kx > 8 ? (h0 ? kx - 8 : 8) : kx;
+  const int k = (kx > 8 && NJ < 4) ? (h0 ? kx - 8 : 8) : kx;
   C1 += (long long)h0 * ldc;
   double *const pout = partial + (long long)(h0 ? nrng : 0) * L * 8 + (long long)rng * L * k;
   auto xcol = [&](int j) { return colp_(X, h0 + j); };
@@ -718,17 +718,23 @@ __global__ __launch_bounds__(16 * RW) void k_nn_tn_w(MvDesc Q, int L, const doub
         if (xprim) *xs = x1;
       }
       lds_barrier();
-      // phase 2: tiles w, w + NWAVE, ... against the RW rows of X1 (staged columns L + j)
+      // phase 2: tiles w, w + NWAVE, ... against the RW rows of X1 (staged columns L + j); a
+      // K step's X1 operands are read once and reused by all of the wave's tiles (LDS reads
+      // per wave and chunk: RW/4 (NJ + TPW) instead of RW/4 TPW (1 + NJ))
+      if (NT_DIAG_MASK & 2) {
 #pragma unroll
-      for (int mm = 0; mm < ((NT_DIAG_MASK & 2) ? TPW : 0); ++mm) {
-        const int tt = w + NWAVE * mm;
-        if (16 * tt < L) {
+        for (int s = 0; s < RW / 4; ++s) {
+          double xb[NJ];
 #pragma unroll
-          for (int s = 0; s < RW / 4; ++s) {
-            const double qa = Qs[(16 * tt + c) * LDQ + 4 * s + g];
+          for (int jg = 0; jg < NJ; ++jg) xb[jg] = Qs[(L + 4 * jg + n4) * LDQ + 4 * s + g];
 #pragma unroll
-            for (int jg = 0; jg < NJ; ++jg)
-              acc2[mm][jg] = mfma4(qa, Qs[(L + 4 * jg + n4) * LDQ + 4 * s + g], acc2[mm][jg]);
+          for (int mm = 0; mm < TPW; ++mm) {
+            const int tt = w + NWAVE * mm;
+            if (16 * tt < L) {
+              const double qa = Qs[(16 * tt + c) * LDQ + 4 * s + g];
+#pragma unroll
+              for (int jg = 0; jg < NJ; ++jg) acc2[mm][jg] = mfma4(qa, xb[jg], acc2[mm][jg]);
+            }
           }
         }
       }
@@ -806,10 +812,16 @@ static int nw_wg_per_cu(int L, int k) {
   const int fit = (int)((160 * 1024) / lds);
   return fit < NW_WG_PER_CU ? fit : NW_WG_PER_CU;
 }
+// k > 8: one workgroup stages each chunk of Q once and forms all k columns (NJ = 4) when its
+// image and C1 fit the LDS (L <= 320 at k = 16); wider images run the two column halves in
+// workgroup pairs on one XCD (paired: every chunk of Q enters two CUs, from HBM once and from
+// L2 / the Infinity Cache once -- twice the bytes into the CUs, which is what bounds it).
+static bool nw_single16(int L, int k) { return k > 8 && k <= 16 && L >= 64 && L + k <= 512 && nw_wg_per_cu(L, k) >= 1; }
 static bool nw_ok(int L, int k) {
-  if (k > 8) return k <= 16 && nw_ok(L, 8);  // column halves in one launch
+  if (k > 8) return k <= 16 && (nw_single16(L, k) || nw_ok(L, 8));  // all columns, or halves in one launch
   return L >= 64 && L + k <= 512 && nw_wg_per_cu(L, k) >= 1;
 }
+bool nn_tn_paired(int L, int k) { return k > 8 && !nw_single16(L, k); }
 
 static int cu_count() {
   static int cus = 0;
@@ -826,8 +838,9 @@ int nn_tn_blocks(int nrows, int L, int k) {
   if (nw_ok(L, k)) {
     const int kh = k > 8 ? 8 : k;
     const long long nchunks = (nrows + NW_RW - 1) / NW_RW;
-    const long long want = (long long)nw_wg_per_cu(L, kh) * cu_count();
-    if (k > 8) {  // pairs of workgroups per chunk range, ranges in groups of 8 (one per XCD)
+    const long long want = (long long)nw_wg_per_cu(L, k > 8 ? k : kh) * cu_count();
+    if (nn_tn_paired(L, k)) {  // pairs of workgroups per chunk range, ranges in groups of 8 (one per XCD)
+      const long long want = (long long)nw_wg_per_cu(L, kh) * cu_count();
       long long r = (want / 2) / 8 * 8;
       if (r > nchunks) r = nchunks / 8 * 8;
       if (r < 8) r = 8;
@@ -855,14 +868,17 @@ void launch_nn_tn(hipStream_t s, MvDesc Q, int L, const double *C1, int ldc, MvD
     throw Error(MIGMRES_EINVAL, "nn_tn: 1 <= k <= 16 and L <= 256 (L + k <= 512 for k <= 8, L >= 64)");
   if (Q.cols) throw Error(MIGMRES_EINVAL, "nn_tn: Q must be a contiguous column range");
   if (nw_ok(L, k)) {
-    if (k > 8 && (nblocks % 16 != 0 || (long long)(nblocks / 2) > ((long long)nrows + NW_RW - 1) / NW_RW + 7))
+    const bool paired = nn_tn_paired(L, k);
+    if (paired && (nblocks % 16 != 0 || (long long)(nblocks / 2) > ((long long)nrows + NW_RW - 1) / NW_RW + 7))
       throw Error(MIGMRES_EINVAL, "nn_tn: k > 8 needs a grid of 16 q workgroups (nn_tn_blocks)");
-    const int NJ = k > 8 ? 2 : (k + 3) >> 2;
-    const int kh = k > 8 ? 8 : k;
+    if (k > 8 && store_x1) throw Error(MIGMRES_EINVAL, "nn_tn: k > 8 is read-only");
+    const int NJ = k > 8 ? (paired ? 2 : 4) : (k + 3) >> 2;
+    const int kh = paired ? 8 : k;
     nt_kernel_t f = store_x1 ? (NJ == 1 ? nw_pick_nm<NW_RW, 1, true>(L + kh) : nw_pick_nm<NW_RW, 2, true>(L + kh))
+                  : NJ == 4  ? nw_pick_nm<NW_RW, 4, false>(L + kh)
                              : (NJ == 1 ? nw_pick_nm<NW_RW, 1, false>(L + kh) : nw_pick_nm<NW_RW, 2, false>(L + kh));
     const size_t lds = nw_lds_bytes<NW_RW>(L, NJ);
-    static bool attr_set[2][2][17] = {};
+    static bool attr_set[2][4][17] = {};
     const int nm = (L + kh + 31) >> 5;
     if (!attr_set[store_x1][NJ - 1][nm]) {
       if (hipFuncSetAttribute((const void *)f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)

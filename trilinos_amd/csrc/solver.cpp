@@ -371,7 +371,8 @@ struct FastIcgs {
     x1_store = xs && xs[0] == '1';
     const size_t np = std::max({(size_t)nblk_tn * 512 * 16, (size_t)nblk_ic * 17,
                                 (size_t)nn_tn_blocks(nl, 16, 1) * 256 * 16,
-                                (size_t)1024 * (size_t)std::min(lmax, 1024) * 8});  // wide nn_tn halves
+                                (size_t)1024 * (size_t)std::min(lmax, 1024) * 8,  // wide nn_tn halves
+                                (size_t)nn_tn_blocks(nl, std::min(std::max(lmax, 64), 320), 16) * 320 * 16});  // k = 16 in one workgroup
     MIG_HIP(hipMalloc(&partial, sizeof(double) * np));
     MIG_HIP(hipMalloc(&R1, sizeof(double) * (size_t)(lmax + k) * k));
     MIG_HIP(hipMalloc(&R2, sizeof(double) * (size_t)(lmax + k) * k));
@@ -499,9 +500,13 @@ struct FastIcgs {
         launch_nn_tn(ctx->stream, Q, L, C1, ldc1, X, n_local, partial, nb, sink, false);
       }
       ProfScope ps(ctx, K_REDUCE, 8.0 * nb / 2 * L * k);
-      launch_reduce_partials_ld(ctx->stream, partial, nb / 2, L, 8, L, 1.0, out);
-      launch_reduce_partials_ld(ctx->stream, partial + (size_t)(nb / 2) * L * 8, nb / 2, L, k - 8, L, 1.0,
-                                out + (size_t)8 * L);
+      if (nn_tn_paired(L, k)) {
+        launch_reduce_partials_ld(ctx->stream, partial, nb / 2, L, 8, L, 1.0, out);
+        launch_reduce_partials_ld(ctx->stream, partial + (size_t)(nb / 2) * L * 8, nb / 2, L, k - 8, L, 1.0,
+                                  out + (size_t)8 * L);
+      } else {
+        launch_reduce_partials_ld(ctx->stream, partial, nb, L, k, L, 1.0, out);
+      }
       allreduce(out, (size_t)L * k);
       return false;
     }
