@@ -173,3 +173,22 @@ def test_distributed_preconditioned_solves(case, P):
     rerun = oracle_case_rerun(gen, n, P, k, params, side, sweeps, damping)
     for first, r in out:
         _check(r, ref, Aor, B, X, rerun)
+
+
+@pytest.mark.parametrize("kind,dims,k,damping", [("Brick3D", (12, 11, 10), 8, 1.0), ("Laplace3D", (13, 12, 11), 4, 0.7),
+                                                 ("Laplace2D", (41, 37, 1), 3, 1.0)])
+def test_fused_right_jacobi_bit_identical(comm, kind, dims, k, damping, monkeypatch):
+    """Right Jacobi (one sweep) fused into the template SpMM forms each operand as
+    (omega D^-1) x exactly like the separate Jacobi kernel: the same solve with
+    MIGMRES_NO_FUSED_JACOBI=1 returns bit-identical solutions, histories and counters."""
+    n, _ = _gen(kind, dims)
+    params = {"Block Size": k, "Num Blocks": 12, "Maximum Iterations": 300, "Maximum Restarts": 30,
+              "Convergence Tolerance": 1e-9, "Orthogonalization": "ICGS"}
+    rng = np.random.default_rng(3)
+    B = rng.standard_normal((n, k))
+    fused = _run_case(comm, n, kind, dims, k, params, "right", 1, damping, B)
+    monkeypatch.setenv("MIGMRES_NO_FUSED_JACOBI", "1")
+    plain = _run_case(comm, n, kind, dims, k, params, "right", 1, damping, B)
+    assert fused[0] == plain[0] and fused[1] == plain[1] and fused[2] == plain[2]
+    assert np.array_equal(fused[3], plain[3])
+    assert np.array_equal(fused[4], plain[4])

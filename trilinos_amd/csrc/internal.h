@@ -82,8 +82,13 @@ void launch_spmm(hipStream_t s, int row_begin, int row_end, const int *rowptr, c
                  MvDesc Y, double alpha, double beta, const int *sel = nullptr, int nsel = 0);
 // Row-pair templates (make_pair_templates): every pair whose template id is not kTplNone;
 // the others are left to one of the kernels above.
+// colscale (optional): Y = alpha A diag(colscale) X + beta Y with diag(colscale) X formed per
+// operand exactly as k_jacobi forms (omega D^-1) X (the right Jacobi preconditioner fused).
 void launch_spmm_tpl(hipStream_t s, int n_local, const unsigned char *tid, const int2 *rec, int ntpl, int maxk,
-                     const double *vals, int nvals, MvDesc X, MvDesc Y, double alpha, double beta);
+                     const double *vals, int nvals, MvDesc X, MvDesc Y, double alpha, double beta,
+                     const double *colscale = nullptr);
+// out[r] = omega * a[r] (r < n)
+void launch_scaled_copy(hipStream_t s, const double *a, double omega, double *out, int n);
 
 // Partial products for C = A^T B over `nrows` rows: writes nblocks x (L*kb) partials.
 int gemm_tn_blocks(int nrows);

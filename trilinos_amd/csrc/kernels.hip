@@ -396,7 +396,8 @@ template <int KC>
 __global__ __launch_bounds__(256) void k_spmm_tpl(int npairs, int n_local, const unsigned char *__restrict__ tid,
                                                   const int2 *__restrict__ rec, int maxk, int nrec,
                                                   const double *__restrict__ vals, int nvals, MvDesc X, MvDesc Y,
-                                                  int c0, int kc, double alpha, double beta) {
+                                                  int c0, int kc, double alpha, double beta,
+                                                  const double *__restrict__ cs) {
 #pragma clang fp contract(off)
   extern __shared__ double tpl_lds[];
   double *s_val = tpl_lds;                   // 256 dictionary slots (255: none, 0.0)
@@ -418,19 +419,26 @@ __global__ __launch_bounds__(256) void k_spmm_tpl(int npairs, int n_local, const
     double sa[KC], sb[KC];
 #pragma unroll
     for (int c = 0; c < KC; ++c) sa[c] = sb[c] = 0.0;
-    d2 xn[KC];
+    d2 xn[KC], scn = d2{1.0, 1.0};
     int2 qn = r[0];
 #pragma unroll
     for (int c = 0; c < KC; ++c) xn[c] = *(const d2 *)(xc[c] + 2LL * (p + qn.x));
+    if (cs) scn = *(const d2 *)(cs + 2LL * (p + qn.x));
     for (int u = 0; u < maxk; ++u) {
       d2 x[KC];
 #pragma unroll
       for (int c = 0; c < KC; ++c) x[c] = xn[c];
+      const d2 sc = scn;
       const unsigned sl = (unsigned)qn.y;
       if (u + 1 < maxk) {  // uniform: issue the next key's loads before these products
         qn = r[u + 1];
 #pragma unroll
         for (int c = 0; c < KC; ++c) xn[c] = *(const d2 *)(xc[c] + 2LL * (p + qn.x));
+        if (cs) scn = *(const d2 *)(cs + 2LL * (p + qn.x));
+      }
+      if (cs) {  // fused Jacobi: the operand is (omega D^-1) x, formed exactly as k_jacobi forms it
+#pragma unroll
+        for (int c = 0; c < KC; ++c) x[c] = sc * x[c];
       }
       const unsigned s0 = sl & 0xFF, s1 = (sl >> 8) & 0xFF, s2 = (sl >> 16) & 0xFF, s3 = sl >> 24;
       const double v0 = s_val[s0], v1 = s_val[s1], v2 = s_val[s2], v3 = s_val[s3];
@@ -476,7 +484,8 @@ template <int KC, int MAXK>
 __global__ __launch_bounds__(256) void k_spmm_tplr(int npairs, int n_local, const unsigned char *__restrict__ tid,
                                                    const int2 *__restrict__ rec, int nrec,
                                                    const double *__restrict__ vals, int nvals, MvDesc X, MvDesc Y,
-                                                   int c0, int kc, double alpha, double beta) {
+                                                   int c0, int kc, double alpha, double beta,
+                                                   const double *__restrict__ cs) {
 #pragma clang fp contract(off)
   extern __shared__ double tpl_lds[];
   double *s_val = tpl_lds;
@@ -503,6 +512,11 @@ __global__ __launch_bounds__(256) void k_spmm_tplr(int npairs, int n_local, cons
     }
     const int ra = 2 * p;
     const bool hasb = ra + 1 < n_local;
+    d2 sc[MAXK];
+    if (cs) {
+#pragma unroll
+      for (int u = 0; u < MAXK; ++u) sc[u] = *(const d2 *)(cs + 2LL * key[u]);
+    }
 #pragma unroll
     for (int c = 0; c < KC; ++c) {
       if (c >= kc) break;
@@ -510,6 +524,10 @@ __global__ __launch_bounds__(256) void k_spmm_tplr(int npairs, int n_local, cons
       d2 x[MAXK];
 #pragma unroll
       for (int u = 0; u < MAXK; ++u) x[u] = *(const d2 *)(xc + 2LL * key[u]);
+      if (cs) {  // fused Jacobi: (omega D^-1) x exactly as k_jacobi forms it
+#pragma unroll
+        for (int u = 0; u < MAXK; ++u) x[u] = sc[u] * x[u];
+      }
       double sa = 0.0, sb = 0.0;
 #pragma unroll
       for (int u = 0; u < MAXK; ++u) {
@@ -566,11 +584,11 @@ static void tpl_launch(K kern, hipStream_t s, size_t lds, int npairs, const void
 template <int KC>
 static void tpl_cols(hipStream_t s, size_t lds, int npairs, int n_local, const unsigned char *tid, const int2 *rec,
                      int maxk, int nrec, const double *vals, int nvals, MvDesc X, MvDesc Y, int c0, int kc,
-                     double alpha, double beta) {
+                     double alpha, double beta, const double *cs) {
 #define TPLR_CASE(K)                                                                                          \
   case K:                                                                                                     \
     tpl_launch([&](int grid) { k_spmm_tplr<KC, K><<<grid, 256, lds, s>>>(npairs, n_local, tid, rec, nrec, vals, \
-                                                                        nvals, X, Y, c0, kc, alpha, beta); }, \
+                                                                        nvals, X, Y, c0, kc, alpha, beta, cs); }, \
                s, lds, npairs, (const void *)k_spmm_tplr<KC, K>);                                             \
     return;
   switch (maxk) {
@@ -591,12 +609,13 @@ static void tpl_cols(hipStream_t s, size_t lds, int npairs, int n_local, const u
   }
 #undef TPLR_CASE
   tpl_launch([&](int grid) { k_spmm_tpl<KC><<<grid, 256, lds, s>>>(npairs, n_local, tid, rec, maxk, nrec, vals, nvals,
-                                                                  X, Y, c0, kc, alpha, beta); },
+                                                                  X, Y, c0, kc, alpha, beta, cs); },
              s, lds, npairs, (const void *)k_spmm_tpl<KC>);
 }
 
 void launch_spmm_tpl(hipStream_t s, int n_local, const unsigned char *tid, const int2 *rec, int ntpl, int maxk,
-                     const double *vals, int nvals, MvDesc X, MvDesc Y, double alpha, double beta) {
+                     const double *vals, int nvals, MvDesc X, MvDesc Y, double alpha, double beta,
+                     const double *colscale) {
   const int npairs = (n_local + 1) / 2;
   if (npairs <= 0) return;
   const int nrec = ntpl * maxk;
@@ -605,13 +624,13 @@ void launch_spmm_tpl(hipStream_t s, int n_local, const unsigned char *tid, const
   for (int c0 = 0; c0 < k; c0 += 8) {
     const int kc = (k - c0) < 8 ? (k - c0) : 8;
     if (kc == 1)
-      tpl_cols<1>(s, lds, npairs, n_local, tid, rec, maxk, nrec, vals, nvals, X, Y, c0, kc, alpha, beta);
+      tpl_cols<1>(s, lds, npairs, n_local, tid, rec, maxk, nrec, vals, nvals, X, Y, c0, kc, alpha, beta, colscale);
     else if (kc <= 2)
-      tpl_cols<2>(s, lds, npairs, n_local, tid, rec, maxk, nrec, vals, nvals, X, Y, c0, kc, alpha, beta);
+      tpl_cols<2>(s, lds, npairs, n_local, tid, rec, maxk, nrec, vals, nvals, X, Y, c0, kc, alpha, beta, colscale);
     else if (kc <= 4)
-      tpl_cols<4>(s, lds, npairs, n_local, tid, rec, maxk, nrec, vals, nvals, X, Y, c0, kc, alpha, beta);
+      tpl_cols<4>(s, lds, npairs, n_local, tid, rec, maxk, nrec, vals, nvals, X, Y, c0, kc, alpha, beta, colscale);
     else
-      tpl_cols<8>(s, lds, npairs, n_local, tid, rec, maxk, nrec, vals, nvals, X, Y, c0, kc, alpha, beta);
+      tpl_cols<8>(s, lds, npairs, n_local, tid, rec, maxk, nrec, vals, nvals, X, Y, c0, kc, alpha, beta, colscale);
     LAUNCH_CHECK();
   }
 }
@@ -1110,6 +1129,17 @@ __global__ __launch_bounds__(256) void k_jacobi(MvDesc X, MvDesc Y, const double
   const double t = (omega * dinv[r]) * colp(X, c)[r];
   double *y = colp(Y, c) + r;
   *y = ACC ? 1.0 * (*y) + t : t;
+}
+
+__global__ __launch_bounds__(256) void k_scaled_copy(const double *__restrict__ a, double omega, double *out, int n) {
+#pragma clang fp contract(off)
+  const long long r = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (r < n) out[r] = omega * a[r];
+}
+void launch_scaled_copy(hipStream_t s, const double *a, double omega, double *out, int n) {
+  if (n <= 0) return;
+  k_scaled_copy<<<cdiv(n, 256), 256, 0, s>>>(a, omega, out, n);
+  LAUNCH_CHECK();
 }
 
 void launch_diag_inv(hipStream_t s, const int *rowptr, const int *cols, const double *vals, int n,

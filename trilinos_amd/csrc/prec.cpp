@@ -8,6 +8,7 @@ using namespace migmres;
 
 migmres_prec::~migmres_prec() {
   if (d_dinv) hipFree(d_dinv);
+  if (d_sdinv) hipFree(d_sdinv);
   delete work;
 }
 
@@ -55,6 +56,11 @@ extern "C" int migmres_jacobi_create(migmres_crs *A, int sweeps, double damping,
     const int n = A->n_local;
     MIG_HIP(hipMalloc(&M->d_dinv, sizeof(double) * (n > 0 ? n : 1)));
     launch_diag_inv(A->ctx->stream, A->d_rowptr, A->d_cols, A->d_vals, n, M->d_dinv);
+    // the fused form's column scale omega * dinv, with two zero entries past n for the row-pair
+    // kernels' reads of a last half-filled pair
+    MIG_HIP(hipMalloc(&M->d_sdinv, sizeof(double) * ((size_t)n + 2)));
+    MIG_HIP(hipMemsetAsync(M->d_sdinv, 0, sizeof(double) * ((size_t)n + 2), A->ctx->stream));
+    launch_scaled_copy(A->ctx->stream, M->d_dinv, damping, M->d_sdinv, n);
     MIG_HIP(hipStreamSynchronize(A->ctx->stream));
     *out = M;
   });

@@ -954,6 +954,20 @@ void crs_apply(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, double alpha,
   }
 }
 
+bool crs_apply_jacobi_fused(migmres_crs &A, const migmres_prec &M, const migmres_mv &X, migmres_mv &Y) {
+  migmres_ctx *c = A.ctx;
+  const int n_remote = (int)A.plan.remote_lids.size();
+  const int n_export = (int)A.export_lids.size();
+  const bool halo = c->nranks > 1 && (n_remote > 0 || n_export > 0);
+  if (!A.use_tpl || A.n_tpl_rest > 0 || halo || M.sweeps != 1 || !M.d_sdinv || M.A != &A) return false;
+  if (X.n_local != A.n_local || Y.n_local != A.n_local || X.ncols != Y.ncols) return false;
+  const int k = X.ncols;
+  ProfScope ps(c, K_SPMM, A.spmm_fixed_bytes + 8.0 * A.n_local * (2.0 * k + 1.0));
+  launch_spmm_tpl(c->stream, A.n_local, A.d_tpl_id, A.d_tpl_rec, A.tpl_ntpl, A.tpl_maxk, A.d_tpl_val, A.tpl_nvals,
+                  X.desc(), Y.desc(), 1.0, 0.0, M.d_sdinv);
+  return true;
+}
+
 }  // namespace migmres
 
 // ------------------------------------------------------------------------------------

@@ -172,6 +172,7 @@ struct migmres_prec {
   migmres_ctx *ctx = nullptr;
   migmres_crs *A = nullptr;
   double *d_dinv = nullptr;
+  double *d_sdinv = nullptr;  // omega * dinv (+2 zero entries): the fused form's column scale
   int sweeps = 1;
   double damping = 1.0;
   long long n_apply = 0;
@@ -204,5 +205,10 @@ migmres_crs *crs_create(migmres_ctx *ctx, long long n_global, long long first, i
                         const long long *rowptr, const long long *gcols, const double *vals);
 // Y = alpha*A*X + beta*Y including the halo import.
 void crs_apply(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, double alpha, double beta);
+// Right Jacobi fused into the operator: Y = A (M X) with M = Ifpack2 Jacobi, one sweep from
+// zero, formed operand by operand inside the template SpMM -- bit-identical to prec_apply
+// followed by crs_apply.  Only where every row pair is templated and no halo is needed;
+// returns false (nothing done) otherwise.
+bool crs_apply_jacobi_fused(migmres_crs &A, const migmres_prec &M, const migmres_mv &X, migmres_mv &Y);
 
 }  // namespace migmres

@@ -917,11 +917,23 @@ struct Problem {
       op(x, t);
       prec(*LP, t, y);
     } else {
+      // right Jacobi fused into the template SpMM where the operator allows it (one launch,
+      // no M x round trip through HBM; same bits); MIGMRES_NO_FUSED_JACOBI=1 disables
+      if (fuse_jacobi && crs_apply_jacobi_fused(*A, *RP, x, y)) {
+        ++RP->n_apply;
+        ++S->n_prec;
+        ++S->n_apply;
+        return;
+      }
       migmres_mv &t = scratch(y.ncols);
       prec(*RP, x, t);
       op(t, y);
     }
   }
+  const bool fuse_jacobi = [] {
+    const char *e = std::getenv("MIGMRES_NO_FUSED_JACOBI");
+    return !(e && e[0] == '1');
+  }();
   // applyRightPrec (BelosLinearProblem.hpp:1103-1114)
   void apply_right_prec(const migmres_mv &x, migmres_mv &y) {
     if (RP)
