@@ -127,6 +127,16 @@ int migmres_plan_pair_templates(int n_local, const long long *rowptr, const int 
 int migmres_crs_create(migmres_ctx *ctx, long long n_global, long long first, int n_local,
                        const long long *rowptr, const long long *gcols, const double *vals,
                        migmres_crs **out);
+/* The same operator from a CSR already in device memory (rowptr_dev: n_local+1 int64 offsets,
+ * gcols_dev: int64 global column ids in insertion order, vals_dev: doubles; all on the
+ * context's device, read only): FillComplete's column map, local ids, sorted rows and the
+ * import's remote lists are built on the device (replaces Epetra_CrsGraph::MakeColMap_int,
+ * epetra/src/Epetra_CrsGraph.cpp:1348-1524; MakeIndicesLocal + SortEntries,
+ * Epetra_CrsMatrix.cpp:1147-1199) and equal migmres_crs_create's.  Rows must not repeat a
+ * column (merge duplicates first, as the file readers do). */
+int migmres_crs_create_device(migmres_ctx *ctx, long long n_global, long long first, int n_local,
+                              const long long *rowptr_dev, const long long *gcols_dev, const double *vals_dev,
+                              migmres_crs **out);
 /* Galeri generators built natively on the host of each rank ("Laplace2D", "Laplace3D",
  * "Brick3D" = the 27-point Xpetra Brick3D with a = 26, b..g = -1); nz ignored for 2-D.
  * "FlanProxy" (not Galeri: a synthetic stand-in of SuiteSparse Flan_1565, 3 dofs per node of

@@ -46,6 +46,7 @@ _SIGS = {
     "migmres_plan_pair_templates": [i32, P(i64), P(i32), P(f64), P(C.c_uint8), P(i32), P(f64), P(i32), P(i32),
                                     P(i32), P(i32)],
     "migmres_crs_create": [vp, i64, i64, i32, P(i64), P(i64), P(f64), P(vp)],
+    "migmres_crs_create_device": [vp, i64, i64, i32, vp, vp, vp, P(vp)],
     "migmres_crs_create_galeri": [vp, C.c_char_p, i32, i32, i32, P(vp)],
     "migmres_crs_destroy": [vp],
     "migmres_matrix_file_info": [C.c_char_p, P(i64), P(i64), P(i32)],

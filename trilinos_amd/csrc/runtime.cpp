@@ -667,6 +667,12 @@ migmres_crs::~migmres_crs() {
 
 namespace migmres {
 
+// The part of crs_create after FillComplete's index maps: export lists, device copies, the
+// SpMM formats and the halo split.  A holds colmap / plan; lcols / lvals are the X-space
+// local CSR (rows sorted by Epetra local id).  d_* arrays already on the device (the device
+// FillComplete's outputs) are kept, otherwise uploaded.
+static void crs_finish(migmres_crs *A, const long long *rowptr, std::vector<int> &lcols, std::vector<double> &lvals);
+
 migmres_crs *crs_create(migmres_ctx *ctx, long long n_global, long long first, int n_local,
                         const long long *rowptr, const long long *gcols, const double *vals) {
   MIG_CHECK(ctx && n_local >= 0 && rowptr, "bad CRS arguments");
@@ -698,6 +704,43 @@ migmres_crs *crs_create(migmres_ctx *ctx, long long n_global, long long first, i
     }
     for (int i = 0; i < n_remote; ++i) xspace[(size_t)p.remote_lids[(size_t)i]] = n_local + i;
     for (auto &v : lcols) v = xspace[(size_t)v];
+    crs_finish(A, rowptr, lcols, lvals);
+  } catch (...) {
+    delete A;
+    throw;
+  }
+  return A;
+}
+
+migmres_crs *crs_create_device(migmres_ctx *ctx, long long n_global, long long first, int n_local,
+                               const long long *d_rowptr, const long long *d_gcols, const double *d_vals) {
+  MIG_CHECK(ctx && n_local >= 0 && d_rowptr, "bad CRS arguments");
+  MIG_HIP(hipSetDevice(ctx->device));
+  auto *A = new migmres_crs();
+  try {
+    A->ctx = ctx;
+    A->n_global = n_global;
+    A->first = first;
+    A->n_local = n_local;
+    std::vector<long long> rowptr;
+    std::vector<int> lcols;
+    std::vector<double> lvals;
+    fill_complete_device(A, d_rowptr, d_gcols, d_vals, rowptr, lcols, lvals);
+    crs_finish(A, rowptr.data(), lcols, lvals);
+  } catch (...) {
+    delete A;
+    throw;
+  }
+  return A;
+}
+
+static void crs_finish(migmres_crs *A, const long long *rowptr, std::vector<int> &lcols, std::vector<double> &lvals) {
+  migmres_ctx *ctx = A->ctx;
+  const long long first = A->first, nnz = A->nnz;
+  const int n_local = A->n_local;
+  {
+    const RemotePlan &p = A->plan;
+    const int n_remote = (int)p.remote_lids.size();
 
     // neighbour groups of the receive side (remote list is grouped by owner PID)
     for (int i = 0; i < n_remote;) {
@@ -752,17 +795,19 @@ migmres_crs *crs_create(migmres_ctx *ctx, long long n_global, long long first, i
         }
       }
     }
-    // device copies
-    std::vector<int> rp32((size_t)n_local + 1);
-    for (int r = 0; r <= n_local; ++r) rp32[(size_t)r] = (int)rowptr[r];
-    MIG_HIP(hipMalloc(&A->d_rowptr, sizeof(int) * (n_local + 1)));
-    MIG_HIP(hipMalloc(&A->d_cols, sizeof(int) * (nnz > 0 ? nnz : 1)));
-    MIG_HIP(hipMalloc(&A->d_vals, sizeof(double) * (nnz + 8)));
-    MIG_HIP(hipMemset(A->d_vals, 0, sizeof(double) * (nnz + 8)));
-    MIG_HIP(hipMemcpy(A->d_rowptr, rp32.data(), sizeof(int) * (n_local + 1), hipMemcpyHostToDevice));
-    if (nnz) {
-      MIG_HIP(hipMemcpy(A->d_cols, lcols.data(), sizeof(int) * nnz, hipMemcpyHostToDevice));
-      MIG_HIP(hipMemcpy(A->d_vals, lvals.data(), sizeof(double) * nnz, hipMemcpyHostToDevice));
+    // device copies (the device FillComplete has made them already)
+    if (!A->d_rowptr) {
+      std::vector<int> rp32((size_t)n_local + 1);
+      for (int r = 0; r <= n_local; ++r) rp32[(size_t)r] = (int)rowptr[r];
+      MIG_HIP(hipMalloc(&A->d_rowptr, sizeof(int) * (n_local + 1)));
+      MIG_HIP(hipMalloc(&A->d_cols, sizeof(int) * (nnz > 0 ? nnz : 1)));
+      MIG_HIP(hipMalloc(&A->d_vals, sizeof(double) * (nnz + 8)));
+      MIG_HIP(hipMemset(A->d_vals, 0, sizeof(double) * (nnz + 8)));
+      MIG_HIP(hipMemcpy(A->d_rowptr, rp32.data(), sizeof(int) * (n_local + 1), hipMemcpyHostToDevice));
+      if (nnz) {
+        MIG_HIP(hipMemcpy(A->d_cols, lcols.data(), sizeof(int) * nnz, hipMemcpyHostToDevice));
+        MIG_HIP(hipMemcpy(A->d_vals, lvals.data(), sizeof(double) * nnz, hipMemcpyHostToDevice));
+      }
     }
     {
       PairPlan pp;
@@ -874,11 +919,7 @@ migmres_crs *crs_create(migmres_ctx *ctx, long long n_global, long long first, i
       upload_groups(A->send_nbrs, A->export_lids.size(), &A->d_export_grp);
     }
     if (n_remote > 0) upload_groups(A->recv_nbrs, (size_t)n_remote, &A->d_remote_grp);
-  } catch (...) {
-    delete A;
-    throw;
   }
-  return A;
 }
 
 void crs_apply(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, double alpha, double beta) {
@@ -1060,6 +1101,12 @@ extern "C" int migmres_crs_create(migmres_ctx *ctx, long long n_global, long lon
                                   const long long *rowptr, const long long *gcols, const double *vals,
                                   migmres_crs **out) {
   return guard([&] { *out = crs_create(ctx, n_global, first, n_local, rowptr, gcols, vals); });
+}
+
+extern "C" int migmres_crs_create_device(migmres_ctx *ctx, long long n_global, long long first, int n_local,
+                                         const long long *rowptr_dev, const long long *gcols_dev,
+                                         const double *vals_dev, migmres_crs **out) {
+  return guard([&] { *out = crs_create_device(ctx, n_global, first, n_local, rowptr_dev, gcols_dev, vals_dev); });
 }
 
 extern "C" int migmres_crs_create_galeri(migmres_ctx *ctx, const char *kind, int nx, int ny, int nz,

@@ -203,6 +203,13 @@ void mv_assign(const migmres_mv &A, migmres_mv &Y);
 
 migmres_crs *crs_create(migmres_ctx *ctx, long long n_global, long long first, int n_local,
                         const long long *rowptr, const long long *gcols, const double *vals);
+// The same operator from a CSR that is already in device memory (global column ids,
+// insertion order; rowptr int64): FillComplete's index maps built on the device
+// (fillcomplete.hip), identical to crs_create's.
+migmres_crs *crs_create_device(migmres_ctx *ctx, long long n_global, long long first, int n_local,
+                               const long long *d_rowptr, const long long *d_gcols, const double *d_vals);
+void fill_complete_device(migmres_crs *A, const long long *d_rowptr, const long long *d_gcols, const double *d_vals,
+                          std::vector<long long> &rowptr, std::vector<int> &lcols, std::vector<double> &lvals);
 // Y = alpha*A*X + beta*Y including the halo import.
 void crs_apply(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, double alpha, double beta);
 // Right Jacobi fused into the operator: Y = A (M X) with M = Ifpack2 Jacobi, one sweep from

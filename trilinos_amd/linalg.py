@@ -137,6 +137,24 @@ class CrsMatrix:
         self.n_remote, self.n_export = nr.value, ne.value
 
     @classmethod
+    def from_device(cls, comm, n_global, rowptr, gcols, vals):
+        """The operator from a CSR already on the GPU (migmres_crs_create_device): FillComplete's
+        column map, local ids and sorted rows are built there.  rowptr / gcols: int64 and vals:
+        float64 torch tensors on the context's device (this rank's rows, global column ids)."""
+        import torch
+        first, n_local = uniform_map(n_global, comm.nranks, comm.rank)
+        for t, dt in ((rowptr, torch.int64), (gcols, torch.int64), (vals, torch.float64)):
+            if t.dtype != dt or not t.is_cuda or not t.is_contiguous():
+                raise ValueError("rowptr/gcols int64 and vals float64 contiguous GPU tensors expected")
+        if rowptr.numel() != n_local + 1:
+            raise ValueError(f"rowptr must have n_local+1 = {n_local + 1} entries")
+        torch.cuda.synchronize(rowptr.device)
+        h = C.c_void_p()
+        call("migmres_crs_create_device", comm.h, n_global, first, n_local, C.c_void_p(rowptr.data_ptr()),
+             C.c_void_p(gcols.data_ptr()), C.c_void_p(vals.data_ptr()), C.byref(h))
+        return cls(comm, n_global, _handle=h)
+
+    @classmethod
     def galeri(cls, comm, kind, nx, ny, nz=1):
         """Galeri::CreateCrsMatrix("Laplace2D"/"Laplace3D"/"Brick3D") on the uniform "Linear"
         map, generated natively on each rank; "FlanProxy" is the synthetic stand-in of config
