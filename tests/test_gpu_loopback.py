@@ -148,3 +148,49 @@ def test_distributed_solve_matches_oracle(kind, dims, k, nb, P, env, monkeypatch
         X[r[4]:r[4] + r[5].shape[0]] = r[5]
     rel = np.linalg.norm(Bh - Aor.apply(X), axis=0) / np.linalg.norm(Bh, axis=0)
     assert rel.max() <= 1e-8 * 1.01
+
+
+@pytest.mark.parametrize("kind,dims,k,P", [("Laplace2D", (5, 1, 1), 2, 7), ("Laplace3D", (3, 2, 1), 3, 8),
+                                           ("Laplace2D", (1, 1, 1), 1, 3)])
+def test_ranks_without_rows(kind, dims, k, P):
+    """More ranks than rows (Epetra's uniform map gives the last ranks zero rows): the
+    distributed SpMM and a Block GMRES solve still equal the oracle; the empty ranks take part
+    in every all-reduce and exchange with nothing to send."""
+    import trilinos_amd as ta
+    from oracle import belos as ob, epetra as oe
+    n, gen = _gen(kind, dims)
+    Aor = oe.DistCrs(gen, n, P)
+    Xe, _ = oe.epetra_random_mv(9, n, k)
+    Bh = Aor.apply(Xe)
+    params = {"Num Blocks": 4, "Block Size": k, "Maximum Iterations": 50, "Maximum Restarts": 5,
+              "Convergence Tolerance": 1e-10, "Orthogonalization": "ICGS"}
+    ref = ob.solve(Aor.apply, Bh, params)
+
+    def rank_fn(comm):
+        first, nloc = ta.uniform_map(n, comm.nranks, comm.rank)
+        A = ta.CrsMatrix.galeri(comm, kind, *dims)
+        Xd = ta.MultiVector(comm, n, k)
+        Xd.upload(Xe[first:first + nloc])
+        Y = ta.MultiVector(comm, n, k)
+        A.apply(Xd, Y)
+        B = ta.MultiVector(comm, n, k)
+        B.upload(Bh[first:first + nloc])
+        X = ta.MultiVector(comm, n, k)
+        X.put_scalar(0.0)
+        lp = ta.LinearProblem(A, X, B)
+        assert lp.setProblem()
+        sm = ta.BlockGmresSolMgr(lp, params)
+        ret = sm.solve()
+        return first, nloc, Y.download(), ret, sm.getNumIters(), X.download()
+
+    res = run_ranks(P, rank_fn)
+    assert any(r[1] == 0 for r in res)
+    Y = np.zeros((n, k))
+    X = np.zeros((n, k))
+    for first, nloc, y, ret, iters, x in res:
+        Y[first:first + nloc] = y
+        X[first:first + nloc] = x
+        assert (ret == ta.Converged) == ref["converged"] and iters == ref["iterations"]
+    assert np.array_equal(Y, Bh)
+    rel = np.linalg.norm(Bh - Aor.apply(X), axis=0) / np.linalg.norm(Bh, axis=0)
+    assert rel.max() <= 1e-10 * 1.01
