@@ -34,8 +34,11 @@ def run_ranks(P, fn):
             comm = ta.Comm(device=0, rank=r, nranks=P, unique_id=uid)
             out[r] = fn(comm)
         except BaseException as e:  # pragma: no cover - reported below
+            import sys
             import traceback
             errs.append(traceback.format_exc())
+            # now, not after the joins: the other ranks may be left waiting in a collective
+            print(f"[rank {r}] {errs[-1]}", file=sys.stderr, flush=True)
             raise
 
     # daemon threads: a rank that fails leaves the others waiting in the loopback barrier
@@ -192,5 +195,8 @@ def test_ranks_without_rows(kind, dims, k, P):
         X[first:first + nloc] = x
         assert (ret == ta.Converged) == ref["converged"] and iters == ref["iterations"]
     assert np.array_equal(Y, Bh)
+    # the 5- and 6-row Krylov spaces collapse (rank-deficient blocks, blkOrthoSing) and the
+    # oracle stops short of the tolerance too: the returned solution must match its residuals
     rel = np.linalg.norm(Bh - Aor.apply(X), axis=0) / np.linalg.norm(Bh, axis=0)
-    assert rel.max() <= 1e-10 * 1.01
+    rel_ref = np.linalg.norm(Bh - Aor.apply(ref["X"]), axis=0) / np.linalg.norm(Bh, axis=0)
+    np.testing.assert_allclose(rel, rel_ref, rtol=1e-6, atol=1e-13)

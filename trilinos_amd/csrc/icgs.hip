@@ -1409,8 +1409,9 @@ void launch_fb_ca(hipStream_t s, MvDesc X, int j, int has_next, const FbPro &pro
   LAUNCH_CHECK_();
 }
 void launch_scale_col(hipStream_t s, MvDesc X, int j, const FbPro &pro, int nrows, int nb) {
-  if (nrows <= 0) return;
-  k_scale_col<<<nb, ICNT, 0, s>>>(X, j, pro, nrows);
+  // launched on a rank that owns no rows too: its prologue applies the pending scalar step,
+  // which every rank must take to keep the device state (and the decisions read from it) equal
+  k_scale_col<<<nb > 0 ? nb : 1, ICNT, 0, s>>>(X, j, pro, nrows);
   LAUNCH_CHECK_();
 }
 void launch_fb_flush(hipStream_t s, const FbPro &pro) {

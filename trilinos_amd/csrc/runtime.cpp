@@ -107,7 +107,10 @@ static void loop_allreduce(migmres_ctx *c, double *d, size_t n, bool max) {
     if (++g.ar_arrived == g.n) {
       std::vector<double> r = g.ar_in[0];
       for (int q = 1; q < g.n; ++q) {
-        MIG_CHECK(g.ar_in[(size_t)q].size() == n, "loopback all-reduce size mismatch");
+        MIG_CHECK(g.ar_in[(size_t)q].size() == n,
+                  "loopback all-reduce size mismatch: rank " + std::to_string(q) + " sent " +
+                      std::to_string(g.ar_in[(size_t)q].size()) + ", rank " + std::to_string(c->rank) + " " +
+                      std::to_string(n));
         for (size_t i = 0; i < n; ++i)
           r[i] = max ? std::max(r[i], g.ar_in[(size_t)q][i]) : r[i] + g.ar_in[(size_t)q][i];
       }
