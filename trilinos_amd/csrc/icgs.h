@@ -95,4 +95,9 @@ void launch_state_reset(hipStream_t s, IcgsState *st, double blk_tol, double sin
 void launch_add_coef(hipStream_t s, const double *C1, int ld1, const double *C2, int ld2, double *out, int ldo,
                      int L, int k);
 
+// Pseudo-block GMRES, batched k = 1 ICGS: M = blockdiag(C1 [+ C2]) (LB = n L rows, n columns,
+// column j keeps rows j L .. j L + L - 1); B[j] = sqrt|dots[j]| and column j of X scaled by 1/B[j].
+void launch_blockdiag(hipStream_t s, const double *C1, const double *C2, int LB, int n, int L, double *M);
+void launch_norm_scale(hipStream_t s, MvDesc X, int nrows, const double *dots, double *B);
+
 }  // namespace migmres

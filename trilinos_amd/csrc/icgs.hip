@@ -450,7 +450,7 @@ __global__ __launch_bounds__(256, 2) void k_nn_tn(MvDesc Q, int L, const double 
     for (int jg = 0; jg < NJ; ++jg) acc2[m][jg] = 0.0;
 
   // loader: Q column lcol + 32 m (clamped to L - 1: duplicates rewrite the same value),
-  // rows lrow, lrow + 1 -- 8 lanes = one 128-B line.  Q is a contiguous column range.
+  // rows lrow, lrow + 1 -- 8 lanes = one 128-B line.  Q may be a column table (a view).
   const int lrow = 2 * (t & 7), lcol = t >> 3;
   const double *qcol[NM];
   int scol[NM];
@@ -458,7 +458,7 @@ __global__ __launch_bounds__(256, 2) void k_nn_tn(MvDesc Q, int L, const double 
   for (int m = 0; m < NM; ++m) {
     const int i = lcol + 32 * m;
     scol[m] = i < L ? i : L - 1;
-    qcol[m] = Q.base + (long long)scol[m] * Q.ld + lrow;
+    qcol[m] = colp_(Q, scol[m]) + lrow;
   }
   // X1 rows: wave w updates rows 4w + (l >> 4), column l & 15 of every chunk (one 8-byte
   // load and one store per lane and chunk, the same in every wave so that the wait counts
@@ -646,7 +646,7 @@ __global__ __launch_bounds__(16 * RW) void k_nn_tn_w(MvDesc Q, int L, const doub
     int i = lcol + 32 * m;
     i = i < LX ? i : LX - 1;
     lsts[m] = i * LDQ + lrow;
-    lsrc[m] = (i < L ? Q.base + (long long)i * Q.ld : xcol(i - L)) + lrow;
+    lsrc[m] = (i < L ? colp_(Q, i) : xcol(i - L)) + lrow;
   }
   // X1 element e = t mod (RW k): row xr of column xj.  Threads t >= RW k repeat an element
   // and store the same value again, so the X1 store is unconditional: a conditional store
@@ -866,7 +866,7 @@ void launch_nn_tn(hipStream_t s, MvDesc Q, int L, const double *C1, int ldc, MvD
   const int k = X.ncols;
   if (!nn_tn_supported(L, k))
     throw Error(MIGMRES_EINVAL, "nn_tn: 1 <= k <= 16 and L <= 256 (L + k <= 512 for k <= 8, L >= 64)");
-  if (Q.cols) throw Error(MIGMRES_EINVAL, "nn_tn: Q must be a contiguous column range");
+
   if (nw_ok(L, k)) {
     const bool paired = nn_tn_paired(L, k);
     if (paired && (nblocks % 16 != 0 || (long long)(nblocks / 2) > ((long long)nrows + NW_RW - 1) / NW_RW + 7))
@@ -2056,6 +2056,46 @@ void launch_fbg_chol(hipStream_t s, const double *partial, int nblocks, int k, i
 void launch_fbg_chol_l(hipStream_t s, const double *gsum, int k, int stage, IcgsState *st, double *w, double gate) {
   if (k < 2 || k > 16) throw Error(MIGMRES_EINVAL, "fbg_chol_l: 2 <= k <= 16");
   k_fbg_chol_l<<<1, 256, 0, s>>>(gsum, k, stage, st, w, gate);
+  LAUNCH_CHECK_();
+}
+
+
+// -------------------------------------------------------------------------------------
+// Batched k = 1 ICGS for pseudo-block GMRES (solver.cpp, PseudoEngine::batched_ortho): the n
+// right-hand sides' bases side by side as one column table QB (n blocks of L columns) and
+// their new vectors as X (n columns).  The block kernels form every cross product QB^T X;
+// right-hand side j keeps its own block (rows j L .. j L + L - 1 of column j), the rest is
+// masked to zero, so each column is projected against its own basis only.
+// -------------------------------------------------------------------------------------
+__global__ void k_blockdiag(const double *__restrict__ C1, const double *__restrict__ C2, int LB, int n, int L,
+                            double *__restrict__ M) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= LB * n) return;
+  const int r = e % LB, j = e / LB;
+  const bool mine = r / L == j;
+  M[e] = mine ? (C2 ? C1[e] + C2[e] : C1[e]) : 0.0;
+}
+void launch_blockdiag(hipStream_t s, const double *C1, const double *C2, int LB, int n, int L, double *M) {
+  k_blockdiag<<<(LB * n + 255) / 256, 256, 0, s>>>(C1, C2, LB, n, L, M);
+  LAUNCH_CHECK_();
+}
+
+// B[j] = sqrt(|dot_j|) (MvNorm) and x_j *= 1 / B[j] when B[j] > 0 (MvScale), as the k = 1
+// branch of projectAndNormalize does it
+__global__ __launch_bounds__(256) void k_norm_scale(MvDesc X, int nrows, const double *__restrict__ dots,
+                                                    double *__restrict__ B) {
+  const int j = blockIdx.y;
+  const double b = sqrt(fabs(dots[j]));
+  if (blockIdx.x == 0 && threadIdx.x == 0) B[j] = b;
+  if (!(fabs(b) > 0.0)) return;
+  const double inv = 1.0 / b;
+  double *x = colp_(X, j);
+  for (long long r = (long long)blockIdx.x * 256 + threadIdx.x; r < nrows; r += (long long)gridDim.x * 256)
+    x[r] = inv * x[r];
+}
+void launch_norm_scale(hipStream_t s, MvDesc X, int nrows, const double *dots, double *B) {
+  const int gx = std::max(1, std::min(1024, (nrows + 255) / 256));
+  k_norm_scale<<<dim3(gx, X.ncols), 256, 0, s>>>(X, nrows, dots, B);
   LAUNCH_CHECK_();
 }
 

@@ -1609,6 +1609,93 @@ struct PseudoEngine : Engine {
     return *f;
   }
 
+  // Batched k = 1 ICGS (blkOrtho1 with two passes, then MvNorm / MvScale) for every right-hand
+  // side in one launch per pass: the bases side by side as one column table, the block
+  // kernels with block-diagonal coefficients (icgs.hip, launch_blockdiag).  Three passes over
+  // the bases (QB^T X; the fused X1 = X - QB M1 with QB^T X1; the closing X - QB (M1 + M2)
+  // with the column dots) instead of three k = 1 chains per right-hand side.
+  // MIGMRES_PSEUDO_BATCHED=0 keeps the per-right-hand-side chains.
+  const bool batched_on = [] {
+    const char *e = std::getenv("MIGMRES_PSEUDO_BATCHED");
+    return !(e && e[0] == '0');
+  }();
+  double *bt_buf = nullptr, *bt_part = nullptr, *bt_sink = nullptr, *bt_host = nullptr;
+  size_t bt_cap = 0, bt_pcap = 0;
+  ~PseudoEngine() {
+    for (double *p : {bt_buf, bt_part, bt_sink})
+      if (p) (void)hipFree(p);
+    if (bt_host) (void)hipHostFree(bt_host);
+  }
+  bool batched_ok(int n, int L) const {
+    return batched_on && device_ortho() && n >= 2 && n <= 8 && n * L <= 512 && nn_tn_supported(n * L, n);
+  }
+  void batched_ortho(PseudoIter &it, int c, const std::vector<int> &vcols) {
+    migmres_ctx *ctx = lp.X->ctx;
+    hipStream_t s = ctx->stream;
+    const int n = (int)it.st.size(), L = c + 1, LB = n * L, nl = lp.X->n_local;
+    std::vector<int> qcols((size_t)LB);
+    for (int i = 0; i < n; ++i)
+      for (int q = 0; q < L; ++q) qcols[(size_t)(i * L + q)] = it.col(it.st[(size_t)i], q);
+    MvPtr QB(mv_view(it.V.p, qcols.data(), LB));
+    MvPtr X(mv_view(it.V.p, vcols.data(), n));
+    const int nblk_tn = gemm_tn_blocks(nl), nblk_nt = nn_tn_blocks(nl, LB, n), nblk_ic = icgs_blocks(nl);
+    const size_t need = (size_t)4 * LB * n + 2 * (size_t)n;
+    if (need > bt_cap) {
+      if (bt_buf) (void)hipFree(bt_buf);
+      if (bt_host) (void)hipHostFree(bt_host);
+      MIG_HIP(hipMalloc(&bt_buf, sizeof(double) * need));
+      MIG_HIP(hipHostMalloc(&bt_host, sizeof(double) * need, hipHostMallocDefault));
+      bt_cap = need;
+    }
+    const size_t pneed = std::max({(size_t)nblk_tn * LB * n, (size_t)nblk_nt * LB * n, (size_t)nblk_ic * (n + 1)});
+    if (pneed > bt_pcap) {
+      if (bt_part) (void)hipFree(bt_part);
+      MIG_HIP(hipMalloc(&bt_part, sizeof(double) * pneed));
+      bt_pcap = pneed;
+    }
+    if (!bt_sink) MIG_HIP(hipMalloc(&bt_sink, sizeof(double) * 1024 * 2048));
+    double *C1 = bt_buf, *C2 = C1 + (size_t)LB * n, *M1 = C2 + (size_t)LB * n, *M = M1 + (size_t)LB * n;
+    double *dots = M + (size_t)LB * n, *Bn = dots + n;
+    {
+      ProfScope ps(ctx, K_GEMM_TN, 8.0 * nl * (LB + n));
+      launch_gemm_tn_partial(s, QB->desc(), LB, X->desc(), n, nl, bt_part, nblk_tn);
+    }
+    {
+      ProfScope ps(ctx, K_REDUCE, 8.0 * nblk_tn * LB * n);
+      launch_reduce_partials_ld(s, bt_part, nblk_tn, LB, n, LB, 1.0, C1);
+    }
+    ctx->allreduce_async(C1, (size_t)LB * n);
+    launch_blockdiag(s, C1, nullptr, LB, n, L, M1);
+    {
+      ProfScope ps(ctx, K_NN_TN, 8.0 * nl * (LB + n));
+      launch_nn_tn(s, QB->desc(), LB, M1, LB, X->desc(), nl, bt_part, nblk_nt, bt_sink, false);
+    }
+    {
+      ProfScope ps(ctx, K_REDUCE, 8.0 * nblk_nt * LB * n);
+      launch_reduce_partials_ld(s, bt_part, nblk_nt, LB, n, LB, 1.0, C2);
+    }
+    ctx->allreduce_async(C2, (size_t)LB * n);
+    launch_blockdiag(s, C1, C2, LB, n, L, M);
+    {
+      ProfScope ps(ctx, K_GEMM_NN_DOT, 8.0 * nl * (LB + 2.0 * n));
+      launch_gemm_nn_dot(s, QB->desc(), LB, M, LB, X->desc(), nl, -1.0, 1.0, 1, X->desc(), bt_part, nblk_ic);
+    }
+    launch_reduce_partials(s, bt_part, nblk_ic, n, 1.0, dots);
+    ctx->allreduce_async(dots, (size_t)n);
+    {
+      ProfScope ps(ctx, K_SCALE, 16.0 * nl * n);
+      launch_norm_scale(s, X->desc(), nl, dots, Bn);
+    }
+    MIG_HIP(hipMemcpyAsync(bt_host, M, sizeof(double) * ((size_t)LB * n + 2 * n), hipMemcpyDeviceToHost, s));
+    MIG_HIP(hipStreamSynchronize(s));
+    const double *Mh = bt_host, *Bh = bt_host + (size_t)LB * n + n;
+    for (int i = 0; i < n; ++i) {
+      PseudoRhs &rs = it.st[(size_t)i];
+      for (int q = 0; q <= c; ++q) it.Hat(rs, q, c) = Mh[(size_t)(i * L + q) + (size_t)i * LB];
+      it.Hat(rs, c + 1, c) = Bh[i];
+    }
+  }
+
   void setup_pseudo_tests(bool has_left) {  // checkStatusTest (:1156-1265)
     seq = S->p.exp_res_test || has_left;
     imp.kind = seq ? ResTest::GEN_IMPLICIT : ResTest::IMP_RES_NORM;
@@ -1688,7 +1775,9 @@ struct PseudoEngine : Engine {
       lp.apply(*U, *AU);
       auto t0 = Clock::now();
       h.assign((size_t)c + 1, 0.0);
-      if (device_ortho()) {
+      if (batched_ok(n, c + 1)) {
+        batched_ortho(it, c, vcols);
+      } else if (device_ortho()) {
         // every right-hand side's ICGS chain on the stream (its own FastIcgs state), one wait
         std::vector<MvPtr> ws, qs;
         for (int i = 0; i < n; ++i) {
