@@ -111,8 +111,12 @@ def _check(res, ref, A, B, X, rerun=None):
     np.testing.assert_allclose(rel, rel_ref, rtol=1e-3, atol=1e-12)
 
 
+@pytest.mark.parametrize("batched", ["1", "0"])
 @pytest.mark.parametrize("case", range(len(CASES)))
-def test_pseudo_block_solves_match_oracle(comm, case):
+def test_pseudo_block_solves_match_oracle(comm, case, batched, monkeypatch):
+    """Both device orthogonalisations: all right-hand sides batched through the block kernels
+    (default) and one k = 1 chain per right-hand side (MIGMRES_PSEUDO_BATCHED=0)."""
+    monkeypatch.setenv("MIGMRES_PSEUDO_BATCHED", batched)
     kind, dims, nrhs, extra, prec = CASES[case]
     n, gen, Xe = _problem(kind, dims, nrhs)
     params = _params(extra)
