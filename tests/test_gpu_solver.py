@@ -341,3 +341,55 @@ def test_gram_findbasis_against_column_passes(comm, monkeypatch, env, k):
         return sm.residualHistory() + (oracle_rerun(ob.solve, Aor.apply, B, params)() - h1)
     _hist_close(sm2.residualHistory(), sm.residualHistory(), drift)
     np.testing.assert_allclose(X2, X, rtol=0, atol=1e-8 * np.abs(X).max())
+
+
+def test_one_rank_rccl_transport(monkeypatch):
+    """The RCCL transport on one GPU: MIGMRES_FORCE_RCCL=1 gives a one-rank context a real RCCL
+    communicator and switches on every distributed code path (the import-plan exchange, the
+    in-place ncclAllReduce of each partial reduction, the all-reduced Gram steps), which two
+    GPUs would otherwise be needed for.  The solve must equal the plain one-rank solve: same
+    counts, histories within the oracle-drift bar, and the oracle's iteration count."""
+    import trilinos_amd as ta
+    from oracle import belos as ob, epetra as oe
+    nx, ny, nz, k = 14, 13, 12, 4
+    n = nx * ny * nz
+    Aor = oe.DistCrs(lambda f, m: oe.laplace3d_rows(nx, ny, nz, f, m), n, 1)
+    Xe, _ = oe.epetra_random_mv(3, n, k)
+    Bh = Aor.apply(Xe)
+    params = {"Block Size": k, "Num Blocks": 8, "Maximum Iterations": 300, "Maximum Restarts": 30,
+              "Convergence Tolerance": 1e-9, "Orthogonalization": "ICGS"}
+    ref = ob.solve(Aor.apply, Bh, params)
+
+    def run(force):
+        if force:
+            monkeypatch.setenv("MIGMRES_FORCE_RCCL", "1")
+        else:
+            monkeypatch.delenv("MIGMRES_FORCE_RCCL", raising=False)
+        comm = ta.Comm(device=0)
+        A = ta.CrsMatrix.galeri(comm, "Laplace3D", nx, ny, nz)
+        B = ta.MultiVector(comm, n, k)
+        B.upload(Bh)
+        X = ta.MultiVector(comm, n, k)
+        X.put_scalar(0.0)
+        lp = ta.LinearProblem(A, X, B)
+        assert lp.setProblem()
+        sm = ta.BlockGmresSolMgr(lp, params)
+        ret = sm.solve()
+        out = (ret, sm.getNumIters(), sm.counters(), sm.residualHistory(), X.download(),
+               comm.sum_all(np.array([1.5, -2.0])))
+        # release everything that holds the context before the context itself
+        for obj in (sm, lp, X, B, A):
+            if hasattr(obj, "close"):
+                obj.close()
+        del sm, lp, X, B, A
+        comm.close()
+        return out
+
+    plain, rccl = run(False), run(True)
+    assert rccl[0] == plain[0] == ta.Converged
+    assert rccl[1] == plain[1] == ref["iterations"]
+    for key in ("applies", "restarts", "explicit_checks"):
+        assert rccl[2][key] == plain[2][key]
+    _hist_close(rccl[3], ref["history"], oracle_rerun(ob.solve, Aor.apply, Bh, params))
+    np.testing.assert_allclose(rccl[4], plain[4], rtol=0, atol=1e-12 * np.abs(plain[4]).max())
+    assert np.array_equal(rccl[5], [1.5, -2.0])

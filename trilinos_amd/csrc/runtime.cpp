@@ -175,7 +175,7 @@ void migmres_ctx::p2p_end() {
 }
 
 void migmres_ctx::allreduce(double *d, size_t n, bool max) {
-  if (nranks == 1 || n == 0) return;
+  if (!dist || n == 0) return;
   auto t0 = std::chrono::steady_clock::now();
   if (loop) {
     loop_allreduce(this, d, n, max);
@@ -302,7 +302,7 @@ void migmres_ctx::pool_trim() {
 }
 
 void migmres_ctx::allreduce_async(double *d, size_t n) {
-  if (nranks == 1 || n == 0) return;
+  if (!dist || n == 0) return;
   if (loop) {
     loop_allreduce(this, d, n, false);
     return;
@@ -331,15 +331,21 @@ extern "C" int migmres_ctx_create(int device, int rank, int nranks, const unsign
     try {
       MIG_HIP(hipSetDevice(device));
       MIG_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-      if (nranks > 1) {
-        MIG_CHECK(uid != nullptr, "unique id required for nranks > 1");
-        if (is_loop_uid(uid)) {
+      const char *fr = std::getenv("MIGMRES_FORCE_RCCL");
+      const bool force = nranks == 1 && fr && fr[0] == '1';
+      if (nranks > 1 || force) {
+        MIG_CHECK(uid != nullptr || force, "unique id required for nranks > 1");
+        if (uid && is_loop_uid(uid)) {
           c->loop = loop_join(uid, nranks);
         } else {
           ncclUniqueId id;
-          std::memcpy(&id, uid, 128);
+          if (force && !uid)
+            MIG_NCCL(ncclGetUniqueId(&id));
+          else
+            std::memcpy(&id, uid, 128);
           MIG_NCCL(ncclCommInitRank(&c->comm, nranks, id, rank));
         }
+        c->dist = true;
         MIG_HIP(hipStreamCreateWithFlags(&c->halo_stream, hipStreamNonBlocking));
         MIG_HIP(hipEventCreateWithFlags(&c->ev_main, hipEventDisableTiming));
         MIG_HIP(hipEventCreateWithFlags(&c->ev_halo, hipEventDisableTiming));
@@ -754,7 +760,7 @@ static void crs_finish(migmres_crs *A, const long long *rowptr, std::vector<int>
     }
     // export lists: every rank tells each owner which GIDs it needs, in its own order
     // (Epetra_MpiDistributor::CreateFromRecvs with Deterministic = true).
-    if (ctx->nranks > 1) {
+    if (ctx->dist) {
       const int P = ctx->nranks;
       std::vector<double> cnt((size_t)P * P, 0.0);
       for (auto &nb : A->recv_nbrs) cnt[(size_t)ctx->rank * P + nb.pid] = nb.count;
@@ -932,7 +938,7 @@ void crs_apply(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, double alpha,
   const int k = X.ncols;
   const int n_remote = (int)A.plan.remote_lids.size();
   const int n_export = (int)A.export_lids.size();
-  const bool halo = c->nranks > 1 && (n_remote > 0 || n_export > 0);
+  const bool halo = c->dist && (n_remote > 0 || n_export > 0);
   auto spmm = [&](const int *sel, int nsel) {
     if (A.use_pairs)
       launch_spmm_pair(c->stream, A.n_local, A.pair_max_keys, A.pair_rmax, A.d_psv, A.d_psk, A.d_psm, X.desc(),
@@ -1002,7 +1008,7 @@ bool crs_apply_jacobi_fused(migmres_crs &A, const migmres_prec &M, const migmres
   migmres_ctx *c = A.ctx;
   const int n_remote = (int)A.plan.remote_lids.size();
   const int n_export = (int)A.export_lids.size();
-  const bool halo = c->nranks > 1 && (n_remote > 0 || n_export > 0);
+  const bool halo = c->dist && (n_remote > 0 || n_export > 0);
   if (!A.use_tpl || A.n_tpl_rest > 0 || halo || M.sweeps != 1 || !M.d_sdinv || M.A != &A) return false;
   if (X.n_local != A.n_local || Y.n_local != A.n_local || X.ncols != Y.ncols) return false;
   const int k = X.ncols;

@@ -35,6 +35,10 @@ struct ProfScope {
 
 struct migmres_ctx {
   int device = 0, rank = 0, nranks = 1;
+  // the distributed code paths are on: nranks > 1, or one rank with a real RCCL communicator
+  // (MIGMRES_FORCE_RCCL=1 at creation: every all-reduce and the import-plan exchange go
+  // through RCCL with a communicator of one, which tests the RCCL transport on one GPU)
+  bool dist = false;
   // profiling state
   bool prof_on = false;
   struct Pending {

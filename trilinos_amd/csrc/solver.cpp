@@ -393,7 +393,7 @@ struct FastIcgs {
   }
 
   void allreduce(double *d, size_t n) {
-    if (ctx->nranks == 1 || n == 0) return;
+    if (!ctx->dist || n == 0) return;
     ctx->allreduce_async(d, n);
   }
 
@@ -433,7 +433,7 @@ struct FastIcgs {
     pend.j = j;
     pend.k = k;
     pend.complete = complete;
-    if (ctx->nranks > 1) {
+    if (ctx->dist) {
       ProfScope ps(ctx, K_REDUCE, 8.0 * nblk_ic * nv);
       launch_reduce_small(ctx->stream, pp, nblk_ic, nv, red);
       allreduce(red, (size_t)nv);
@@ -607,7 +607,7 @@ struct FastIcgs {
         launch_reduce_partials(ctx->stream, gb.part, nb, nv, 1.0, gb.sum);
         allreduce(gb.sum, (size_t)nv);
         launch_fbg_chol_l(ctx->stream, gb.sum, k, stage, st, gb.w, gate);
-      } else if (ctx->nranks > 1) {
+      } else if (ctx->dist) {
         launch_fbg_chol(ctx->stream, gb.part, nb, k, 0, st, gb.w, gate, gb.sum);
         allreduce(gb.sum, (size_t)nv);
         launch_fbg_chol(ctx->stream, gb.sum, 1, k, stage, st, gb.w, gate, nullptr);
