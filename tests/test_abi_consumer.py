@@ -39,3 +39,26 @@ def test_mvop_tester_and_solve_on_gpu():
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "MVOPTESTER PASSED" in r.stdout and "SOLVE PASSED" in r.stdout
+
+
+EX = os.path.join(DIR, "block_gmres_galeri_ex")
+
+
+@pytest.mark.gpu
+def test_galeri_example_driver_reproduces_reference_run():
+    """tests/abi_consumer/block_gmres_galeri_ex.cpp -- the reference's
+    BlockGmresEpetraGaleriEx.cpp flow written against include/migmres.h in C++ -- run with the
+    recorded reference run's options (--nx=64 --num-rhs=8 --block-size=8
+    --ortho=ICGS --tol=1e-8 --max-subspace=50 --max-restarts=50): the same 201 iterations,
+    268 operator applications (267 in the solve + B = A Xexact), 4 restarts, 61 explicit
+    residual checks and true residuals 3.5e-10 .. 9.9e-9 as the reference printed."""
+    assert os.path.exists(EX), "build first: make -C tests/abi_consumer (done by __graft_entry__.build())"
+    r = subprocess.run([EX, "--nx=64", "--num-rhs=8", "--block-size=8", "--ortho=ICGS", "--tol=1e-8",
+                        "--max-subspace=50", "--max-restarts=50"], capture_output=True, text=True, timeout=120)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "End Result: TEST PASSED" in r.stdout
+    assert "Number of iterations: 201" in r.stdout
+    assert "Operator applications: 267" in r.stdout
+    assert "Restarts: 4" in r.stdout and "Explicit residual checks: 61" in r.stdout
+    assert "True relative residuals: min 3.5e-10 max 9.9e-09" in r.stdout
