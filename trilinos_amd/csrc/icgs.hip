@@ -588,9 +588,13 @@ __global__ __launch_bounds__(256, 2) void k_nn_tn(MvDesc Q, int L, const double 
 // Workgroup b owns the contiguous chunk range [c0, c1): consecutive visits to a column are
 // adjacent pieces (tools/mb_stream.hip, 32-row chunks: 6.0-6.3 TB/s in this order against
 // 5.8-5.9 TB/s grid-stride).
+// RW = 16 with an image of at most 7 x 32 columns (LX = L + k) keeps C1 in registers instead
+// (see k_nn_tn_w), so its LDS is the image + red only.
 template <int RW>
-static size_t nw_lds_bytes(int L, int NJ) {
-  const int Lp = (L + 4 * NJ + 15) & ~15, Lq = (L + 15) & ~15;
+static constexpr bool nw_creg(int NM) { return RW == 16 && NM <= 7; }
+template <int RW>
+static size_t nw_lds_bytes(int L, int NJ, int LX = 0) {
+  const int Lp = (L + 4 * NJ + 15) & ~15, Lq = nw_creg<RW>((LX + 31) >> 5) ? 0 : (L + 15) & ~15;
   return sizeof(double) * ((size_t)Lp * (RW + 1) + (RW / 4) * NJ * 64 + (size_t)Lq * 4 * NJ);
 }
 
@@ -624,9 +628,27 @@ __global__ __launch_bounds__(16 * RW) void k_nn_tn_w(MvDesc Q, int L, const doub
   const int t = threadIdx.x, w = t >> 6, l = t & 63, c = l & 15, g = l >> 4, n4 = l & 3;
   const int rb = w % RB, kq = w / RB;
   for (int e = t; e < Lp * LDQ; e += NTH) Qs[e] = 0.0;
-  for (int e = t; e < Lq * 4 * NJ; e += NTH) {
-    const int i = e / (4 * NJ), j = e % (4 * NJ);
-    C1s[e] = (i < L && j < k) ? C1[i + (long long)j * ldc] : 0.0;
+  // RW = 16, NM <= 7: phase 1's B operands are the same for every chunk (wave kq takes K
+  // steps kq, kq + 4, ...), so each lane keeps its C1 entries in registers -- 4 of the 5 LDS
+  // reads per phase-1 MFMA step at k = 16.  Wider images would need more than the 256
+  // registers per lane that two waves per SIMD leave (2 NM x 4 doubles of C1 alone).
+  constexpr bool CREG = nw_creg<RW>(NM);
+  double c1r[CREG ? 2 * NM : 1][NJ];
+  if constexpr (CREG) {
+#pragma unroll
+    for (int m = 0; m < 2 * NM; ++m) {
+      const int i = 4 * (kq + 4 * m) + g;
+#pragma unroll
+      for (int jg = 0; jg < NJ; ++jg) {
+        const int j = 4 * jg + n4;
+        c1r[m][jg] = (i < L && j < k) ? C1[i + (long long)j * ldc] : 0.0;
+      }
+    }
+  } else {
+    for (int e = t; e < Lq * 4 * NJ; e += NTH) {
+      const int i = e / (4 * NJ), j = e % (4 * NJ);
+      C1s[e] = (i < L && j < k) ? C1[i + (long long)j * ldc] : 0.0;
+    }
   }
   // 16-column tiles of the staged image: 2 NM (L + k <= 32 NM), shared round-robin by the waves
   constexpr int NTILE = 2 * NM, TPW = (NTILE + NWAVE - 1) / NWAVE;
@@ -704,7 +726,8 @@ __global__ __launch_bounds__(16 * RW) void k_nn_tn_w(MvDesc Q, int L, const doub
         if (4 * s < L) {
           const double qa = Qs[(4 * s + g) * LDQ + 16 * rb + c];
 #pragma unroll
-          for (int jg = 0; jg < NJ; ++jg) a1[jg] = mfma4(qa, C1s[(4 * s + g) * 4 * NJ + 4 * jg + n4], a1[jg]);
+          for (int jg = 0; jg < NJ; ++jg)
+            a1[jg] = mfma4(qa, CREG ? c1r[CREG ? m : 0][jg] : C1s[(4 * s + g) * 4 * NJ + 4 * jg + n4], a1[jg]);
         }
       }
 #pragma unroll
@@ -807,9 +830,51 @@ static nt_kernel_t nw_pick_nm(int LX) {
 // The wide variant wins from L = 64 on (256^3, k = 8); below that the per-chunk latency
 // is not hidden.  Up to L + k = 256 NW_WG_PER_CU workgroups' LDS fit in 160 KiB; wider
 // images (k = 16 in column halves: L up to 400 at Num Blocks 25) run one workgroup per CU.
+// k > 8 with all columns in one workgroup can also run on 16-row chunks (256 threads): the
+// image takes half the LDS, so two workgroups share a CU up to L = 256 and one barrier-bound
+// workgroup's MFMA phases overlap the other's loads; and it fits one workgroup up to
+// L + k = 512, so no column-half pairs are needed.  Measured at 256^3, k = 16
+// (tools/mb_k16.cpp, same box): L = 192 7.20 -> 6.58 ms, L = 256 9.16 -> 8.39 ms (two
+// workgroups per CU instead of one), L = 400 20.4 (pairs) -> 18.4 ms; but one 16-row
+// workgroup per CU where the 32-row one also fits once is slower (L = 272: 13.0 vs 9.6 ms),
+// and so is L <= 128 (two 32-row workgroups fit already).  MIGMRES_NW16: 0 off, 1 (default)
+// those two cases, 2 every k > 8 shape.
+static int nw16_mode() {
+  static int m = -1;
+  if (m < 0) {
+    const char *e = std::getenv("MIGMRES_NW16");
+    m = e ? std::atoi(e) : 1;
+  }
+  return m;
+}
+// Resident 16-row workgroups per CU (LDS and the registers that hold C1), at most 2.
+static int nw16_per_cu(int L, int k) {
+  static int cache[513] = {};
+  int &v = cache[L + k];
+  if (!v) {
+    int per_cu = 0;
+    const nt_kernel_t f = nw_pick_nm<16, 4, false>(L + k);
+    if (hipFuncSetAttribute((const void *)f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, 256, nw_lds_bytes<16>(L, 4, L + k)) != hipSuccess)
+      per_cu = 1;
+    v = per_cu < 1 ? -1 : per_cu > 2 ? 2 : per_cu;
+  }
+  return v < 0 ? 0 : v;
+}
+static int nw_rw(int L, int k) {
+  if (k > 8 && k <= 16 && L >= 64 && L + k <= 512) {
+    const int m = nw16_mode();
+    if (m >= 2) return 16;
+    if (m == 1) {
+      const int fit32 = (int)((160 * 1024) / nw_lds_bytes<NW_RW>(L, 4));
+      if ((fit32 == 1 && nw16_per_cu(L, k) >= 2) || fit32 == 0) return 16;
+    }
+  }
+  return NW_RW;
+}
 static int nw_wg_per_cu(int L, int k) {
-  const size_t lds = nw_lds_bytes<NW_RW>(L, (k + 3) >> 2);
-  const int fit = (int)((160 * 1024) / lds);
+  if (nw_rw(L, k) == 16) return nw16_per_cu(L, k);
+  const int fit = (int)((160 * 1024) / nw_lds_bytes<NW_RW>(L, (k + 3) >> 2));
   return fit < NW_WG_PER_CU ? fit : NW_WG_PER_CU;
 }
 // k > 8: one workgroup stages each chunk of Q once and forms all k columns (NJ = 4) when its
@@ -837,7 +902,8 @@ static int cu_count() {
 int nn_tn_blocks(int nrows, int L, int k) {
   if (nw_ok(L, k)) {
     const int kh = k > 8 ? 8 : k;
-    const long long nchunks = (nrows + NW_RW - 1) / NW_RW;
+    const int rw = nw_rw(L, k);
+    const long long nchunks = (nrows + rw - 1) / rw;
     const long long want = (long long)nw_wg_per_cu(L, k > 8 ? k : kh) * cu_count();
     if (nn_tn_paired(L, k)) {  // pairs of workgroups per chunk range, ranges in groups of 8 (one per XCD)
       const long long want = (long long)nw_wg_per_cu(L, kh) * cu_count();
@@ -874,6 +940,20 @@ void launch_nn_tn(hipStream_t s, MvDesc Q, int L, const double *C1, int ldc, MvD
     if (k > 8 && store_x1) throw Error(MIGMRES_EINVAL, "nn_tn: k > 8 is read-only");
     const int NJ = k > 8 ? (paired ? 2 : 4) : (k + 3) >> 2;
     const int kh = paired ? 8 : k;
+    if (nw_rw(L, k) == 16) {
+      nt_kernel_t f = nw_pick_nm<16, 4, false>(L + kh);
+      static bool attr16[17] = {};
+      const int nm = (L + kh + 31) >> 5;
+      if (!attr16[nm]) {
+        if (hipFuncSetAttribute((const void *)f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+          throw Error(MIGMRES_EHIP, "nn_tn: cannot raise the dynamic LDS limit");
+        attr16[nm] = true;
+      }
+      hipLaunchKernelGGL(f, dim3(nblocks), dim3(16 * 16), nw_lds_bytes<16>(L, 4, L + kh), s, Q, L, C1, ldc, X, k, nrows,
+                         partial, sink);
+      LAUNCH_CHECK_();
+      return;
+    }
     nt_kernel_t f = store_x1 ? (NJ == 1 ? nw_pick_nm<NW_RW, 1, true>(L + kh) : nw_pick_nm<NW_RW, 2, true>(L + kh))
                   : NJ == 4  ? nw_pick_nm<NW_RW, 4, false>(L + kh)
                              : (NJ == 1 ? nw_pick_nm<NW_RW, 1, false>(L + kh) : nw_pick_nm<NW_RW, 2, false>(L + kh));

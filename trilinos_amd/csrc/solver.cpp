@@ -369,10 +369,11 @@ struct FastIcgs {
     fb_rev = !(fr && fr[0] == '0');
     const char *xs = std::getenv("MIGMRES_NN_TN_STORE");
     x1_store = xs && xs[0] == '1';
-    const size_t np = std::max({(size_t)nblk_tn * 512 * 16, (size_t)nblk_ic * 17,
-                                (size_t)nn_tn_blocks(nl, 16, 1) * 256 * 16,
-                                (size_t)1024 * (size_t)std::min(lmax, 1024) * 8,  // wide nn_tn halves
-                                (size_t)nn_tn_blocks(nl, std::min(std::max(lmax, 64), 320), 16) * 320 * 16});  // k = 16 in one workgroup
+    size_t np = std::max({(size_t)nblk_tn * 512 * 16, (size_t)nblk_ic * 17,
+                          (size_t)nn_tn_blocks(nl, 16, 1) * 256 * 16,
+                          (size_t)1024 * (size_t)std::min(lmax, 1024) * 8});  // wide nn_tn halves
+    for (int L = 64; L <= std::min(lmax, 512); L += 16)  // k = 16 in one workgroup (16- or 32-row chunks)
+      if (nn_tn_supported(L, 16)) np = std::max(np, (size_t)nn_tn_blocks(nl, L, 16) * L * 16);
     MIG_HIP(hipMalloc(&partial, sizeof(double) * np));
     MIG_HIP(hipMalloc(&R1, sizeof(double) * (size_t)(lmax + k) * k));
     MIG_HIP(hipMalloc(&R2, sizeof(double) * (size_t)(lmax + k) * k));
