@@ -590,19 +590,23 @@ __global__ __launch_bounds__(256, 2) void k_nn_tn(MvDesc Q, int L, const double 
 // 5.8-5.9 TB/s grid-stride).
 // RW = 16 with an image of at most 7 x 32 columns (LX = L + k) keeps C1 in registers instead
 // (see k_nn_tn_w), so its LDS is the image + red only.
-template <int RW>
-static constexpr bool nw_creg(int NM) { return RW == 16 && NM <= 7; }
-template <int RW>
+// The 512-thread variant on 16-row chunks (NT = 512) always does: its 8 waves split phase 1's K
+// in eighths, so each lane holds half as many C1 entries.
+template <int RW, int NT = 16 * RW>
+static constexpr bool nw_creg(int NM) { return RW == 16 && (NT == 512 || NM <= 7); }
+template <int RW, int NT = 16 * RW>
 static size_t nw_lds_bytes(int L, int NJ, int LX = 0) {
-  const int Lp = (L + 4 * NJ + 15) & ~15, Lq = nw_creg<RW>((LX + 31) >> 5) ? 0 : (L + 15) & ~15;
-  return sizeof(double) * ((size_t)Lp * (RW + 1) + (RW / 4) * NJ * 64 + (size_t)Lq * 4 * NJ);
+  const int Lp = (L + 4 * NJ + 15) & ~15, Lq = nw_creg<RW, NT>((LX + 31) >> 5) ? 0 : (L + 15) & ~15;
+  return sizeof(double) * ((size_t)Lp * (RW + 1) + (NT / 64) * NJ * 64 + (size_t)Lq * 4 * NJ);
 }
 
-template <int RW, int NM, int NJ, bool ST>
-__global__ __launch_bounds__(16 * RW) void k_nn_tn_w(MvDesc Q, int L, const double *__restrict__ C1, int ldc,
-                                                     MvDesc X, int kx, int nrows, double *__restrict__ partial,
-                                                     double *__restrict__ sink) {
-  constexpr int NTH = 16 * RW, NWAVE = NTH / 64, RB = RW / 16, LDQ = RW + 1, LPC = RW / 2;
+template <int RW, int NM, int NJ, bool ST, int NT = 16 * RW>
+__global__ __launch_bounds__(NT) void k_nn_tn_w(MvDesc Q, int L, const double *__restrict__ C1, int ldc,
+                                                MvDesc X, int kx, int nrows, double *__restrict__ partial,
+                                                double *__restrict__ sink) {
+  // NT threads: 16 RW (phase 1 in K quarters) or, for RW = 16, 512 (K eighths: KQ = 8)
+  constexpr int NTH = NT, NWAVE = NTH / 64, RB = RW / 16, KQ = NWAVE / RB, LDQ = RW + 1, LPC = RW / 2;
+  constexpr int CPR = NTH / LPC, NLD = (32 * NM + CPR - 1) / CPR, MS = (8 * NM + KQ - 1) / KQ;
   extern __shared__ __attribute__((aligned(16))) double sm[];
   // kx > 8: workgroup pairs take the two column halves of X (columns h0 .. h0 + k - 1) over
   // the same chunk range at the same time and on the same XCD (blocks 16 q + x and
@@ -632,12 +636,12 @@ __global__ __launch_bounds__(16 * RW) void k_nn_tn_w(MvDesc Q, int L, const doub
   // steps kq, kq + 4, ...), so each lane keeps its C1 entries in registers -- 4 of the 5 LDS
   // reads per phase-1 MFMA step at k = 16.  Wider images would need more than the 256
   // registers per lane that two waves per SIMD leave (2 NM x 4 doubles of C1 alone).
-  constexpr bool CREG = nw_creg<RW>(NM);
-  double c1r[CREG ? 2 * NM : 1][NJ];
+  constexpr bool CREG = nw_creg<RW, NT>(NM);
+  double c1r[CREG ? MS : 1][NJ];
   if constexpr (CREG) {
 #pragma unroll
-    for (int m = 0; m < 2 * NM; ++m) {
-      const int i = 4 * (kq + 4 * m) + g;
+    for (int m = 0; m < MS; ++m) {
+      const int i = 4 * (kq + KQ * m) + g;
 #pragma unroll
       for (int jg = 0; jg < NJ; ++jg) {
         const int j = 4 * jg + n4;
@@ -661,11 +665,11 @@ __global__ __launch_bounds__(16 * RW) void k_nn_tn_w(MvDesc Q, int L, const doub
   // loader: staged column lcol + 32 m (clamped to LX - 1: duplicates rewrite the same
   // value), rows lrow, lrow + 1 of the chunk; staged columns >= L come from X.
   const int lrow = 2 * (t % LPC), lcol = t / LPC;
-  const double *lsrc[NM];
-  int lsts[NM];
+  const double *lsrc[NLD];
+  int lsts[NLD];
 #pragma unroll
-  for (int m = 0; m < NM; ++m) {
-    int i = lcol + 32 * m;
+  for (int m = 0; m < NLD; ++m) {
+    int i = lcol + CPR * m;
     i = i < LX ? i : LX - 1;
     lsts[m] = i * LDQ + lrow;
     lsrc[m] = (i < L ? colp_(Q, i) : xcol(i - L)) + lrow;
@@ -689,9 +693,9 @@ __global__ __launch_bounds__(16 * RW) void k_nn_tn_w(MvDesc Q, int L, const doub
   // 2-deep prefetch at one workgroup per CU measured no faster: at large L the kernel is
   // bound by its LDS reads -- about 200 ds_read_b64 per wave per chunk -- not by latency.)
   auto clampc = [&](long long chunk) { return chunk < c1 ? chunk : c1 - 1; };
-  d2 p[NM];
+  d2 p[NLD];
 #pragma unroll
-  for (int m = 0; m < NM; ++m) p[m] = *(const d2 *)(lsrc[m] + (c0 < c1 ? c0 : nchunks - 1) * RW);  // empty range (k > 8, few chunks): any valid chunk
+  for (int m = 0; m < NLD; ++m) p[m] = *(const d2 *)(lsrc[m] + (c0 < c1 ? c0 : nchunks - 1) * RW);  // empty range (k > 8, few chunks): any valid chunk
   // A store behind the prologue loads, like the X1 store behind the in-loop prefetch: the
   // loop header then sees the same pending-event order on both incoming edges and waits
   // vmcnt(1) for the last prefetched column instead of vmcnt(0) (which waits for the X1
@@ -701,7 +705,7 @@ __global__ __launch_bounds__(16 * RW) void k_nn_tn_w(MvDesc Q, int L, const doub
     {
       const long long r0 = ch * RW;
 #pragma unroll
-      for (int m = 0; m < NM; ++m) {
+      for (int m = 0; m < NLD; ++m) {
         if (NT_DIAG_MASK & 4) {
           Qs[lsts[m]] = p[m].x;
           Qs[lsts[m] + 1] = p[m].y;
@@ -713,16 +717,16 @@ __global__ __launch_bounds__(16 * RW) void k_nn_tn_w(MvDesc Q, int L, const doub
       {
         const long long cn = clampc(ch + 1) * RW;
 #pragma unroll
-        for (int m = 0; m < NM; ++m) p[m] = *(const d2 *)(lsrc[m] + cn);
+        for (int m = 0; m < NLD; ++m) p[m] = *(const d2 *)(lsrc[m] + cn);
       }
       const double xval = *xs;
-      // phase 1: rows 16 rb .. 16 rb + 15, K steps s = kq + 4 m (4 s < L <= 32 NM)
+      // phase 1: rows 16 rb .. 16 rb + 15, K steps s = kq + KQ m (4 s < L <= 32 NM)
       double a1[NJ];
 #pragma unroll
       for (int jg = 0; jg < NJ; ++jg) a1[jg] = 0.0;
 #pragma unroll
-      for (int m = 0; m < ((NT_DIAG_MASK & 1) ? 2 * NM : 0); ++m) {
-        const int s = kq + 4 * m;
+      for (int m = 0; m < ((NT_DIAG_MASK & 1) ? MS : 0); ++m) {
+        const int s = kq + KQ * m;
         if (4 * s < L) {
           const double qa = Qs[(4 * s + g) * LDQ + 16 * rb + c];
 #pragma unroll
@@ -734,8 +738,9 @@ __global__ __launch_bounds__(16 * RW) void k_nn_tn_w(MvDesc Q, int L, const doub
       for (int jg = 0; jg < NJ; ++jg) red[((kq * RB + rb) * NJ + jg) * 64 + l] = a1[jg];
       lds_barrier();
       {
-        const double d = (red[((0 * RB + xrb) * NJ + xjg) * 64 + xo] + red[((1 * RB + xrb) * NJ + xjg) * 64 + xo]) +
-                         (red[((2 * RB + xrb) * NJ + xjg) * 64 + xo] + red[((3 * RB + xrb) * NJ + xjg) * 64 + xo]);
+        auto rd = [&](int q) { return red[((q * RB + xrb) * NJ + xjg) * 64 + xo]; };
+        double d = (rd(0) + rd(1)) + (rd(2) + rd(3));
+        if constexpr (KQ == 8) d += (rd(4) + rd(5)) + (rd(6) + rd(7));
         const double x1 = xval - d;
         if ((NT_DIAG_MASK & 8) && ST) xdst[r0 + xr] = x1;
         if (xprim) *xs = x1;
@@ -813,16 +818,16 @@ static nt_kernel_t nt_pick(int L, int k) {
 constexpr int NW_RW = NT_WIDE_RW;  // rows per chunk of the wide variant (32: 2 WGs/CU, 64: 1 WG/CU)
 constexpr int NW_WG_PER_CU = NT_WIDE_WGCU;
 
-template <int RW, int NJ, bool ST>
+template <int RW, int NJ, bool ST, int NT = 16 * RW>
 static nt_kernel_t nw_pick_nm(int LX) {
   switch ((LX + 31) >> 5) {
 #define NW_CASE(N) \
   case N:          \
-    return k_nn_tn_w<RW, N, NJ, ST>;
+    return k_nn_tn_w<RW, N, NJ, ST, NT>;
     NW_CASE(1) NW_CASE(2) NW_CASE(3) NW_CASE(4) NW_CASE(5) NW_CASE(6) NW_CASE(7) NW_CASE(8)
     NW_CASE(9) NW_CASE(10) NW_CASE(11) NW_CASE(12) NW_CASE(13) NW_CASE(14) NW_CASE(15)
 #undef NW_CASE
-    default: return k_nn_tn_w<RW, 16, NJ, ST>;
+    default: return k_nn_tn_w<RW, 16, NJ, ST, NT>;
   }
 }
 
@@ -838,7 +843,7 @@ static nt_kernel_t nw_pick_nm(int LX) {
 // workgroups per CU instead of one), L = 400 20.4 (pairs) -> 18.4 ms; but one 16-row
 // workgroup per CU where the 32-row one also fits once is slower (L = 272: 13.0 vs 9.6 ms),
 // and so is L <= 128 (two 32-row workgroups fit already).  MIGMRES_NW16: 0 off, 1 (default)
-// those two cases, 2 every k > 8 shape.
+// those two cases, 2 every k > 8 shape, 3 every k > 8 shape with 512 threads.
 static int nw16_mode() {
   static int m = -1;
   if (m < 0) {
@@ -847,20 +852,32 @@ static int nw16_mode() {
   }
   return m;
 }
-// Resident 16-row workgroups per CU (LDS and the registers that hold C1), at most 2.
-static int nw16_per_cu(int L, int k) {
+// Resident 16-row workgroups of NT threads per CU (LDS and the registers that hold C1), at most 2.
+template <int NT>
+static int nw16_occ(int L, int k) {
   static int cache[513] = {};
   int &v = cache[L + k];
   if (!v) {
     int per_cu = 0;
-    const nt_kernel_t f = nw_pick_nm<16, 4, false>(L + k);
+    const nt_kernel_t f = nw_pick_nm<16, 4, false, NT>(L + k);
     if (hipFuncSetAttribute((const void *)f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, 256, nw_lds_bytes<16>(L, 4, L + k)) != hipSuccess)
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, NT, nw_lds_bytes<16, NT>(L, 4, L + k)) != hipSuccess)
       per_cu = 1;
     v = per_cu < 1 ? -1 : per_cu > 2 ? 2 : per_cu;
   }
   return v < 0 ? 0 : v;
 }
+// 16-row chunks: 256 threads, or 512 where the 32-row image does not fit the LDS (mode 1) or
+// always (MIGMRES_NW16=3).  Measured (tools/mb_k16.cpp, k = 16, same box): L = 400 18.4 ms
+// (256) -> 13.3 ms (512) against 20.4 ms for the column-half pairs; L = 352 equal; at
+// L <= 272 the 256-thread / 32-row choices are 2-20 % faster.
+static int nw16_threads(int L, int k) {
+  const int m = nw16_mode();
+  if (m == 3) return 512;
+  if (m == 1 && (160 * 1024) / nw_lds_bytes<NW_RW>(L, 4) == 0) return 512;
+  return 256;
+}
+static int nw16_per_cu(int L, int k) { return nw16_threads(L, k) == 512 ? nw16_occ<512>(L, k) : nw16_occ<256>(L, k); }
 static int nw_rw(int L, int k) {
   if (k > 8 && k <= 16 && L >= 64 && L + k <= 512) {
     const int m = nw16_mode();
@@ -941,15 +958,17 @@ void launch_nn_tn(hipStream_t s, MvDesc Q, int L, const double *C1, int ldc, MvD
     const int NJ = k > 8 ? (paired ? 2 : 4) : (k + 3) >> 2;
     const int kh = paired ? 8 : k;
     if (nw_rw(L, k) == 16) {
-      nt_kernel_t f = nw_pick_nm<16, 4, false>(L + kh);
-      static bool attr16[17] = {};
+      const bool t512 = nw16_threads(L, k) == 512;
+      nt_kernel_t f = t512 ? nw_pick_nm<16, 4, false, 512>(L + kh) : nw_pick_nm<16, 4, false>(L + kh);
+      static bool attr16[2][17] = {};
       const int nm = (L + kh + 31) >> 5;
-      if (!attr16[nm]) {
+      if (!attr16[t512][nm]) {
         if (hipFuncSetAttribute((const void *)f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
           throw Error(MIGMRES_EHIP, "nn_tn: cannot raise the dynamic LDS limit");
-        attr16[nm] = true;
+        attr16[t512][nm] = true;
       }
-      hipLaunchKernelGGL(f, dim3(nblocks), dim3(16 * 16), nw_lds_bytes<16>(L, 4, L + kh), s, Q, L, C1, ldc, X, k, nrows,
+      const size_t lds16 = t512 ? nw_lds_bytes<16, 512>(L, 4, L + kh) : nw_lds_bytes<16>(L, 4, L + kh);
+      hipLaunchKernelGGL(f, dim3(nblocks), dim3(t512 ? 512 : 256), lds16, s, Q, L, C1, ldc, X, k, nrows,
                          partial, sink);
       LAUNCH_CHECK_();
       return;
