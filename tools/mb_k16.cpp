@@ -62,7 +62,7 @@ int main(int argc, char **argv) {
   CK(hipDeviceSynchronize());
   hipStream_t s = 0;
   const int nblk = gemm_tn_blocks((int)n);
-  for (int k : {16}) {
+  for (int k : {8, 16}) {
     for (int L : {64, 128, 160, 192, 208, 224, 256, 272, 320, 336, 352, 400}) {
       if (L + k > Lmax) continue;
       MvDesc A{V, ld, nullptr, L + k};

@@ -687,38 +687,33 @@ __global__ __launch_bounds__(NT) void k_nn_tn_w(MvDesc Q, int L, const double *_
   const long long nchunks = (nrows + RW - 1) / RW;
   const long long c0 = nchunks * rng / nrng, c1 = nchunks * (rng + 1) / nrng;
 
-  // 1-deep register prefetch: the next chunk's loads are issued right after the barrier
-  // that publishes the current one and stay in flight through both phases.  Rows past nrows
-  // are zero padding in Q and X, so their X1 is zero and is stored back unguarded.  (A
-  // 2-deep prefetch at one workgroup per CU measured no faster: at large L the kernel is
-  // bound by its LDS reads -- about 200 ds_read_b64 per wave per chunk -- not by latency.)
+  // (A 2-deep prefetch measured no faster: for the 32-row, C1-in-LDS form at one workgroup
+  // per CU, where the LDS reads -- about 200 ds_read_b64 per wave per chunk -- bound it, and
+  // for the 512-thread 16-row form at k = 16, L = 128 .. 400, chunks in pairs.)
   auto clampc = [&](long long chunk) { return chunk < c1 ? chunk : c1 - 1; };
-  d2 p[NLD];
-#pragma unroll
-  for (int m = 0; m < NLD; ++m) p[m] = *(const d2 *)(lsrc[m] + (c0 < c1 ? c0 : nchunks - 1) * RW);  // empty range (k > 8, few chunks): any valid chunk
   // A store behind the prologue loads, like the X1 store behind the in-loop prefetch: the
   // loop header then sees the same pending-event order on both incoming edges and waits
   // vmcnt(1) for the last prefetched column instead of vmcnt(0) (which waits for the X1
   // store's completion).  partial[0] of this workgroup is rewritten at the end.
-  if ((NT_DIAG_MASK & 8) && ST) pout[0] = 0.0;
-  for (long long ch = c0; ch < c1; ++ch) {
+  // One chunk: publish the prefetched image pp, refill pp with chunk `nxt`, both phases.
+  auto body = [&](d2(&pp)[NLD], long long ch, long long nxt) {
+    const long long r0 = ch * RW;
+#pragma unroll
+    for (int m = 0; m < NLD; ++m) {
+      if (NT_DIAG_MASK & 4) {
+        Qs[lsts[m]] = pp[m].x;
+        Qs[lsts[m] + 1] = pp[m].y;
+      } else if (pp[m].x == 12345.0) {
+        Qs[0] = pp[m].y;
+      }
+    }
+    lds_barrier();
     {
-      const long long r0 = ch * RW;
+      const long long cn = clampc(nxt) * RW;
 #pragma unroll
-      for (int m = 0; m < NLD; ++m) {
-        if (NT_DIAG_MASK & 4) {
-          Qs[lsts[m]] = p[m].x;
-          Qs[lsts[m] + 1] = p[m].y;
-        } else if (p[m].x == 12345.0) {
-          Qs[0] = p[m].y;
-        }
-      }
-      lds_barrier();
-      {
-        const long long cn = clampc(ch + 1) * RW;
-#pragma unroll
-        for (int m = 0; m < NLD; ++m) p[m] = *(const d2 *)(lsrc[m] + cn);
-      }
+      for (int m = 0; m < NLD; ++m) pp[m] = *(const d2 *)(lsrc[m] + cn);
+    }
+    if (ch < c1) {
       const double xval = *xs;
       // phase 1: rows 16 rb .. 16 rb + 15, K steps s = kq + KQ m (4 s < L <= 32 NM)
       double a1[NJ];
@@ -766,8 +761,19 @@ __global__ __launch_bounds__(NT) void k_nn_tn_w(MvDesc Q, int L, const double *_
           }
         }
       }
-      lds_barrier();
     }
+    lds_barrier();
+  };
+  const long long cf = c0 < c1 ? c0 : nchunks - 1;  // empty range (k > 8, few chunks): any valid chunk
+  {
+    // 1-deep register prefetch: the next chunk's loads are issued right after the barrier
+    // that publishes the current one and stay in flight through both phases.  Rows past nrows
+    // are zero padding in Q and X, so their X1 is zero and is stored back unguarded.
+    d2 p[NLD];
+#pragma unroll
+    for (int m = 0; m < NLD; ++m) p[m] = *(const d2 *)(lsrc[m] + cf * RW);
+    if ((NT_DIAG_MASK & 8) && ST) pout[0] = 0.0;
+    for (long long ch = c0; ch < c1; ++ch) body(p, ch, ch + 1);
   }
   // partial (L x k) of this workgroup: tile tt rows 16 tt + 4 b + m
   double *out = pout;
