@@ -90,9 +90,10 @@ def test_config_solves_match_oracle(comm, case):
 def test_k16_full_cycle_matches_oracle(comm, dims, nb, P):
     """Config 3's block size through a whole long cycle (tol 1e-15: never converges, so every
     block step runs): L = 16 .. 16 (nb - 1), which takes the fused update + projection through
-    both of its k = 16 forms -- all 16 columns in one workgroup (L <= 320) and the column
-    halves in workgroup pairs (L = 336, 352, 368) -- and the Gram-form findBasis at k = 16;
-    counts and residual history against the oracle."""
+    each of its k = 16 forms in the default selection (MIGMRES_NW16=1) -- 32-row chunks (L = 64
+    .. 128 and 272 .. 336), 16-row chunks in two 256-thread workgroups per CU (L = 160 .. 256;
+    C1 in registers up to L = 208) and 512-thread 16-row workgroups (L = 352, 368) -- and the
+    Gram-form findBasis at k = 16; counts and residual history against the oracle."""
     import trilinos_amd as ta
     k = 16
     params = _params(k, nb, **{"Convergence Tolerance": 1e-15, "Maximum Iterations": nb, "Maximum Restarts": 0})
