@@ -130,7 +130,10 @@ def main():
     ap.add_argument("--cpu-iters", type=int, default=0, help="cpu_baseline block iterations (0: one cycle)")
     # secondary workloads; the defaults are the headline configuration
     ap.add_argument("--solver", default="BLOCK GMRES", choices=["BLOCK GMRES", "FLEXIBLE GMRES", "GMRES"])
-    ap.add_argument("--matrix", default="Laplace3D", choices=["Laplace3D", "Brick3D"])
+    ap.add_argument("--matrix", default="Laplace3D", choices=["Laplace3D", "Brick3D", "FlanProxy"],
+                    help="FlanProxy: configs[3]'s shape (Flan_1565 is not in this image) -- 81 x 81 x 80 "
+                         "hexahedral nodes x 3 dofs = 1,574,640 rows, ~73 nnz per row, unstructured SELL path; "
+                         "--nx is ignored")
     ap.add_argument("--matrix-file", default=None,
                     help="MatrixMarket / Harwell-Boeing file (configs[3]: SuiteSparse Flan_1565 .mtx, not in this "
                          "image) read natively by every rank; overrides --matrix/--nx")
@@ -161,6 +164,10 @@ def main():
     if args.matrix_file:
         A = ta.CrsMatrix.read_file(comm, args.matrix_file)
         n = A.n_global
+    elif args.matrix == "FlanProxy":
+        dims = (81, 81, 80)
+        n = 3 * dims[0] * dims[1] * dims[2]
+        A = ta.CrsMatrix.galeri(comm, "FlanProxy", *dims)
     else:
         n = nx ** 3
         A = ta.CrsMatrix.galeri(comm, args.matrix, nx, nx, nx)
@@ -234,7 +241,9 @@ def main():
     model_bytes = iteration_bytes_model(n, nnz_total, k, nb, steps)
     headline = (args.solver == "BLOCK GMRES" and args.matrix == "Laplace3D" and args.prec == "none"
                 and args.ortho == "ICGS" and not args.matrix_file and nx == 256 and k == 8 and nb == 25)
-    mname = os.path.basename(args.matrix_file) if args.matrix_file else f"{args.matrix} n={nx}^3"
+    mname = (os.path.basename(args.matrix_file) if args.matrix_file else
+             f"FlanProxy n={n} (synthetic stand-in for SuiteSparse Flan_1565)" if args.matrix == "FlanProxy" else
+             f"{args.matrix} n={nx}^3")
     wl = (f"3-D 7-pt Laplacian n={nx}^3 fp64, k={k} RHS, Block GMRES Num Blocks {nb}, ICGS, fixed work (tol 0)"
           if headline else
           f"{mname} fp64, k={k} RHS, {args.solver} Num Blocks {nb}, {args.ortho}, "
