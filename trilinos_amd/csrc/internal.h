@@ -74,9 +74,11 @@ void launch_spmm_pair(hipStream_t s, int n_local, int max_keys, int rmax, const 
                       const unsigned short *sm, MvDesc X, const double *ghost, long long ldg, MvDesc Y,
                       double alpha, double beta, const int *sel = nullptr, int nsel = 0);
 // General rows: thread per row over the SELL-64 copy (make_sell64); sel lists rows.
+// xr (optional, n_local x 8 doubles): scratch for a row-interleaved copy of X's owned rows,
+// so each entry's k operands are one contiguous segment instead of k column gathers.
 void launch_spmm_sell(hipStream_t s, int n_local, const long long *off, const int *len, const int *scol,
                       const double *sval, MvDesc X, const double *ghost, long long ldg, MvDesc Y, double alpha,
-                      double beta, const int *sel = nullptr, int nsel = 0);
+                      double beta, const int *sel = nullptr, int nsel = 0, double *xr = nullptr);
 void launch_spmm(hipStream_t s, int row_begin, int row_end, const int *rowptr, const int *cols,
                  const double *vals, MvDesc X, int n_local, const double *ghost, long long ldg,
                  MvDesc Y, double alpha, double beta, const int *sel = nullptr, int nsel = 0);

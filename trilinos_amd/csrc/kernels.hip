@@ -134,13 +134,17 @@ void launch_spmm(hipStream_t s, int row_begin, int row_end, const int *rowptr, c
 // column-index / value load of a wave is one contiguous 256 / 512-byte segment.  Sums in
 // stored order, products v * x, no FMA: bit-identical to k_spmm and the reference loop.
 // -------------------------------------------------------------------------------------
-template <int KC>
+// XR: the owned operands come from xr, a row-interleaved copy of X's columns c0 .. c0 + KC - 1
+// (k_interleave): one entry's KC values are KC / 2 16-byte loads of one 8 KC-byte segment
+// (one cache line) instead of KC 8-byte gathers from KC lines.  Same values, same order.
+template <int KC, bool XR = false>
 __global__ __launch_bounds__(256) void k_spmm_sell(int n, const long long *__restrict__ off,
                                                    const int *__restrict__ len, const int *__restrict__ scol,
                                                    const double *__restrict__ sval, MvDesc X, int n_local,
                                                    const double *__restrict__ ghost, long long ldg, MvDesc Y,
                                                    int c0, int kc, double alpha, double beta,
-                                                   const int *__restrict__ sel, int nsel) {
+                                                   const int *__restrict__ sel, int nsel,
+                                                   const double *__restrict__ xr = nullptr) {
 #pragma clang fp contract(off)
   constexpr int J = KC >= 4 ? 4 : 8;  // entries whose KC x loads are issued together
   const int t = blockIdx.x * 256 + threadIdx.x;
@@ -182,8 +186,23 @@ __global__ __launch_bounds__(256) void k_spmm_sell(int n, const long long *__res
       for (int j = 0; j < J; ++j) {
         const int col = ci[j0 + j];
         const bool own = col < n_local;
+        if constexpr (XR) {
+          if (own) {
+            const d2 *xp = (const d2 *)(xr + (long long)col * KC);
 #pragma unroll
-        for (int c = 0; c < KC; ++c) xv[j][c] = *(own ? xc[c] + col : gc[c] + (col - n_local));
+            for (int h = 0; h < KC / 2; ++h) {
+              const d2 q = xp[h];
+              xv[j][2 * h] = q.x;
+              xv[j][2 * h + 1] = q.y;
+            }
+          } else {
+#pragma unroll
+            for (int c = 0; c < KC; ++c) xv[j][c] = gc[c][col - n_local];
+          }
+        } else {
+#pragma unroll
+          for (int c = 0; c < KC; ++c) xv[j][c] = *(own ? xc[c] + col : gc[c] + (col - n_local));
+        }
       }
       asm volatile("" ::: "memory");
 #pragma unroll
@@ -209,15 +228,45 @@ __global__ __launch_bounds__(256) void k_spmm_sell(int n, const long long *__res
   }
 }
 
+// xr[r][c] = X[r][c0 + c] for c < kc, 0 beyond (KC-wide rows)
+template <int KC>
+__global__ __launch_bounds__(256) void k_interleave(MvDesc X, int c0, int kc, int n, double *__restrict__ xr) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= n) return;
+  double v[KC];
+#pragma unroll
+  for (int c = 0; c < KC; ++c) v[c] = c < kc ? colp(X, c0 + c)[r] : 0.0;
+  d2 *out = (d2 *)(xr + (long long)r * KC);
+#pragma unroll
+  for (int h = 0; h < KC / 2; ++h) out[h] = d2{v[2 * h], v[2 * h + 1]};
+}
+
 void launch_spmm_sell(hipStream_t s, int n_local, const long long *off, const int *len, const int *scol,
                       const double *sval, MvDesc X, const double *ghost, long long ldg, MvDesc Y, double alpha,
-                      double beta, const int *sel, int nsel) {
+                      double beta, const int *sel, int nsel, double *xr) {
   const int n = sel ? nsel : n_local;
   if (n <= 0) return;
   const int k = Y.ncols;
   const dim3 grid(cdiv(n, 256));
   for (int c0 = 0; c0 < k; c0 += 8) {
     const int kc = (k - c0) < 8 ? (k - c0) : 8;
+    if (xr && kc >= 2) {
+      const dim3 gi(cdiv(n_local, 256));
+#define SELL_XR(KC)                                                                                            \
+  k_interleave<KC><<<gi, 256, 0, s>>>(X, c0, kc, n_local, xr);                                               \
+  k_spmm_sell<KC, true><<<grid, 256, 0, s>>>(n_local, off, len, scol, sval, X, n_local, ghost, ldg, Y, c0, kc, \
+                                             alpha, beta, sel, nsel, xr);
+      if (kc <= 2) {
+        SELL_XR(2)
+      } else if (kc <= 4) {
+        SELL_XR(4)
+      } else {
+        SELL_XR(8)
+      }
+#undef SELL_XR
+      LAUNCH_CHECK();
+      continue;
+    }
     if (kc == 1)
       k_spmm_sell<1><<<grid, 256, 0, s>>>(n_local, off, len, scol, sval, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel);
     else if (kc <= 2)

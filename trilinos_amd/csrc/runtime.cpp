@@ -663,7 +663,7 @@ void mv_assign(const migmres_mv &A, migmres_mv &Y) {
 // distributed CRS operator
 // ------------------------------------------------------------------------------------
 migmres_crs::~migmres_crs() {
-  for (void *p : {(void *)d_soff, (void *)d_slen, (void *)d_scol, (void *)d_sval, (void *)d_tpl_id,
+  for (void *p : {(void *)d_soff, (void *)d_slen, (void *)d_scol, (void *)d_sval, (void *)d_xr, (void *)d_tpl_id,
                   (void *)d_tpl_rec, (void *)d_tpl_val, (void *)d_tpl_rest})
     if (p) hipFree(p);
   for (void *p : {(void *)d_export_grp, (void *)d_remote_grp, (void *)d_recv})
@@ -735,6 +735,7 @@ migmres_crs *crs_create_device(migmres_ctx *ctx, long long n_global, long long f
     std::vector<int> lcols;
     std::vector<double> lvals;
     fill_complete_device(A, d_rowptr, d_gcols, d_vals, rowptr, lcols, lvals);
+    if (!A->nnz && (int)rowptr.size() > n_local) A->nnz = rowptr[(size_t)n_local];
     crs_finish(A, rowptr.data(), lcols, lvals);
   } catch (...) {
     delete A;
@@ -939,13 +940,28 @@ void crs_apply(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, double alpha,
   const int n_remote = (int)A.plan.remote_lids.size();
   const int n_export = (int)A.export_lids.size();
   const bool halo = c->dist && (n_remote > 0 || n_export > 0);
+  // SELL with k >= 2: operands through a row-interleaved copy of X (MIGMRES_NO_SELL_XR=1: column
+  // gathers).  Measured at the bench shapes (same box): FlanProxy (73 nnz/row) k = 4 SpMM 0.604 ->
+  // 0.483 ms, k = 8 464 -> 585 it/s; Brick3D (27 nnz/row, gathers already line-local) k = 4 1.93 ->
+  // 1.90 ms but k = 8 3.22 -> 3.53 ms (the 8-column copy costs more than it saves) -- so up to 4
+  // columns, or any width for long rows.  Not for the few template-rest rows.
+  static const bool sell_xr = [] {
+    const char *e = std::getenv("MIGMRES_NO_SELL_XR");
+    return !(e && e[0] == '1');
+  }();
+  double *xr = nullptr;
+  if (A.use_sell && !A.use_pairs && !A.use_tpl && sell_xr && k >= 2 && A.n_local > 0 &&
+      (k <= 4 || A.nnz >= 48LL * A.n_local)) {
+    if (!A.d_xr) MIG_HIP(hipMalloc(&A.d_xr, sizeof(double) * 8 * (size_t)A.n_local));
+    xr = A.d_xr;
+  }
   auto spmm = [&](const int *sel, int nsel) {
     if (A.use_pairs)
       launch_spmm_pair(c->stream, A.n_local, A.pair_max_keys, A.pair_rmax, A.d_psv, A.d_psk, A.d_psm, X.desc(),
                        A.d_ghost, A.ldg, Y.desc(), alpha, beta, sel, nsel);
     else if (A.use_sell)
       launch_spmm_sell(c->stream, A.n_local, A.d_soff, A.d_slen, A.d_scol, A.d_sval, X.desc(), A.d_ghost, A.ldg,
-                       Y.desc(), alpha, beta, sel, nsel);
+                       Y.desc(), alpha, beta, sel, nsel, xr);
     else
       launch_spmm(c->stream, 0, A.n_local, A.d_rowptr, A.d_cols, A.d_vals, X.desc(), A.n_local, A.d_ghost, A.ldg,
                   Y.desc(), alpha, beta, sel, nsel);

@@ -148,6 +148,7 @@ struct migmres_crs {
   int *d_slen = nullptr, *d_scol = nullptr;
   double *d_sval = nullptr;
   bool use_sell = false;
+  double *d_xr = nullptr;  // SELL: row-interleaved copy of X's owned rows (n_local x 8), on first apply with k >= 2
   // row-pair templates (k_spmm_tpl) when the pairs repeat a few shapes: templated pairs run
   // there (reading no ghost column, they also make the interior half of the halo overlap);
   // the rest -- pairs that read a ghost column -- go to the kernel above through
