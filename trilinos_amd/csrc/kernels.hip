@@ -134,9 +134,6 @@ void launch_spmm(hipStream_t s, int row_begin, int row_end, const int *rowptr, c
 // column-index / value load of a wave is one contiguous 256 / 512-byte segment.  Sums in
 // stored order, products v * x, no FMA: bit-identical to k_spmm and the reference loop.
 // -------------------------------------------------------------------------------------
-#ifndef SELL_XR_J8
-#define SELL_XR_J8 0
-#endif
 // XR: the owned operands come from xr, a row-interleaved copy of X's columns c0 .. c0 + KC - 1
 // (k_interleave): one entry's KC values are KC / 2 16-byte loads of one 8 KC-byte segment
 // (one cache line) instead of KC 8-byte gathers from KC lines.  Same values, same order.
@@ -149,8 +146,9 @@ __global__ __launch_bounds__(256) void k_spmm_sell(int n, const long long *__res
                                                    const int *__restrict__ sel, int nsel,
                                                    const double *__restrict__ xr = nullptr) {
 #pragma clang fp contract(off)
-  // entries whose KC x loads are issued together (XR: KC / 2 16-byte loads per entry)
-  constexpr int J = (KC >= 4 && !(XR && SELL_XR_J8)) ? 4 : 8;
+  // entries whose KC x loads are issued together (XR: KC / 2 16-byte loads per entry; 8
+  // entries at a time there measured the same as 4 on FlanProxy)
+  constexpr int J = KC >= 4 ? 4 : 8;
   const int t = blockIdx.x * 256 + threadIdx.x;
   int r;
   if (sel) {
