@@ -138,9 +138,12 @@ def test_config_solves_distributed(case, P):
         _check(r, ref, Aor, B, X, rerun)
 
 
-@pytest.mark.parametrize("dims,k,P", [((9, 8, 7), 4, 1), ((9, 8, 7), 4, 3), ((13, 7, 5), 7, 2)])
+@pytest.mark.parametrize("dims,k,P", [((9, 8, 7), 4, 1), ((9, 8, 7), 4, 3), ((13, 7, 5), 7, 2),
+                                      ((9, 8, 7), 2, 1), ((9, 8, 7), 3, 2), ((12, 11, 10), 12, 1)])
 def test_flan_proxy_spmm_bit_exact(dims, k, P):
-    """The general (SELL-64) kernel on the unstructured rows, P = 1 and with ghost columns."""
+    """The general (SELL-64) kernel on the unstructured rows, P = 1 and with ghost columns,
+    through the row-interleaved X copy (k <= 4: 2- and 4-wide rows, k = 3 padded; k = 12: an
+    8-column chunk -- interleaved where the rows average >= 48 entries -- then a 4-column one)."""
     import trilinos_amd as ta
     from oracle import epetra as oe
     n, gen = _gen("FlanProxy", dims)
