@@ -139,7 +139,7 @@ def test_config_solves_distributed(case, P):
 
 
 @pytest.mark.parametrize("dims,k,P", [((9, 8, 7), 4, 1), ((9, 8, 7), 4, 3), ((13, 7, 5), 7, 2),
-                                      ((9, 8, 7), 2, 1), ((9, 8, 7), 3, 2), ((12, 11, 10), 12, 1)])
+                                      ((9, 8, 7), 2, 1), ((9, 8, 7), 3, 2), ((13, 11, 10), 12, 1)])
 def test_flan_proxy_spmm_bit_exact(dims, k, P):
     """The general (SELL-64) kernel on the unstructured rows, P = 1 and with ghost columns,
     through the row-interleaved X copy (k <= 4: 2- and 4-wide rows, k = 3 padded; k = 12: an
