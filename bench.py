@@ -58,7 +58,7 @@ def cpu_baseline(k, nb, m, iters):
     tol 0 -- for `iters` block iterations (one whole restart cycle by default) with
     OMP_NUM_THREADS threads.  With m < 256 the rate is scaled by rows (m^3 / 256^3) and says so."""
     import ctypes as C
-    so = os.path.join(ROOT, "oracle", "_ref", "libcport.so")
+    so = os.path.join(ROOT, "oracle", "cport", "libcport.so")
     lib = C.CDLL(so)
     secs = (C.c_double * 2)()
     nh = C.c_int()
@@ -72,6 +72,20 @@ def cpu_baseline(k, nb, m, iters):
     if m != 256:
         sample += f", scaled by {m}^3/256^3 rows to the 256^3 workload"
     return {"value": val, "unit": "iterations/s", "cores": int(secs[1]), "kind": "port", "sample": sample}
+
+
+def cpu_baseline_subprocess(threads, k, nb, m, iters, timeout=300):
+    """cpu_baseline with OMP_NUM_THREADS=`threads` in a child process (the OpenMP runtime
+    reads it once, at start-up).  The child loads only the C restatement, never the GPU."""
+    import subprocess
+    code = ("import sys, json; sys.path.insert(0, %r); import bench; "
+            "print(json.dumps(bench.cpu_baseline(%d, %d, %d, %d)))" % (ROOT, k, nb, m, iters))
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads))
+    try:
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=timeout)
+        return json.loads(r.stdout.strip().splitlines()[-1])
+    except Exception as e:  # the baseline is reported, not required
+        return {"value": None, "error": f"{type(e).__name__}: {e}"}
 
 
 def pmc_ratio(kernel_class, world):
@@ -91,11 +105,15 @@ def pmc_ratio(kernel_class, world):
         return None
 
 
-def spawn_ranks(n, argv, port=None):
+def spawn_ranks(n, argv, port=None, timeout=None, poll_s=0.1):
     """`bench.py --gpus N` without a torchrun environment: start N rank processes of this
     script (one per GPU, RANK = LOCAL_RANK = i, WORLD_SIZE = N, MASTER_ADDR 127.0.0.1) as
-    children, before anything in this process touches the GPU, and return the first non-zero
-    exit code (0 when every rank succeeded).  Rank 0 prints the JSON line."""
+    children, before anything in this process touches the GPU.  Every child is polled: on
+    the first non-zero exit the others are terminated (then killed after 10 s) and that exit
+    code is returned, so a rank that dies (RCCL init, out of memory, bad device) cannot leave
+    its peers blocked in a collective.  Past `timeout` seconds every rank is killed and 124
+    is returned.  0 when every rank succeeded.  Rank 0 prints the JSON line."""
+    import signal
     import socket
     import subprocess
     if port is None:
@@ -108,12 +126,56 @@ def spawn_ranks(n, argv, port=None):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen(argv, env=env))
-    rc = 0
-    for p in procs:
-        c = p.wait()
-        if c != 0 and rc == 0:
-            rc = c
-    return rc
+
+    def stop_all():
+        live = [p for p in procs if p.poll() is None]
+        for p in live:
+            p.send_signal(signal.SIGTERM)
+        t_end = time.monotonic() + 10.0
+        for p in live:
+            try:
+                p.wait(timeout=max(0.1, t_end - time.monotonic()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+
+    t0 = time.monotonic()
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+            if bad:
+                r, c = bad[0]
+                print(f"bench.py: rank {r} exited with status {c}; stopping the other ranks", file=sys.stderr,
+                      flush=True)
+                stop_all()
+                return c
+            if all(c == 0 for c in codes):
+                return 0
+            if timeout is not None and time.monotonic() - t0 > timeout:
+                print(f"bench.py: ranks still running after {timeout} s; stopping them", file=sys.stderr, flush=True)
+                stop_all()
+                return 124
+            time.sleep(poll_s)
+    except BaseException:
+        stop_all()
+        raise
+
+
+def start_watchdog(seconds, rank):
+    """A hang anywhere in a rank (a collective whose peer died after joining, a stuck device
+    call) ends the rank with status 124 after `seconds`, so the launcher (spawn_ranks or
+    torchrun's agent) stops the job and reports instead of waiting for its own time limit."""
+    import threading
+
+    def fire():
+        print(f"bench.py: rank {rank} still running after {seconds} s; exiting (124)", file=sys.stderr, flush=True)
+        os._exit(124)
+
+    t = threading.Timer(seconds, fire)
+    t.daemon = True
+    t.start()
+    return t
 
 
 def main():
@@ -126,6 +188,7 @@ def main():
     ap.add_argument("--nb", type=int, default=25)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--no-cpu-one-core", action="store_true", help="skip the 1-core cpu_baseline sample")
     ap.add_argument("--cpu-nx", type=int, default=256, help="cpu_baseline sample size (m^3 rows)")
     ap.add_argument("--cpu-iters", type=int, default=0, help="cpu_baseline block iterations (0: one cycle)")
     # secondary workloads; the defaults are the headline configuration
@@ -140,10 +203,15 @@ def main():
     ap.add_argument("--prec", default="none", choices=["none", "right", "left"])
     ap.add_argument("--sweeps", type=int, default=1)
     ap.add_argument("--ortho", default="ICGS", choices=["ICGS", "DGKS"])
+    ap.add_argument("--comm-timeout", type=float, default=300.0,
+                    help="seconds: torch.distributed (gloo) set-up / barrier timeout and the RCCL init watchdog")
+    ap.add_argument("--deadline", type=float, default=1500.0,
+                    help="seconds: a rank still running after this exits with status 124 (N > 1; 0 = off)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        sys.exit(spawn_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]))
+        sys.exit(spawn_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                             timeout=args.deadline + 60 if args.deadline > 0 else None))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
@@ -152,12 +220,25 @@ def main():
     import torch
     import torch.distributed as dist
     if world > 1:
+        if args.deadline > 0:
+            start_watchdog(args.deadline, rank)
+        # one GPU per rank: check before set_device (device_count does not initialise HIP)
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+        ndev = torch.cuda.device_count()
+        if ndev < local_world or local >= ndev:
+            sys.exit(f"bench.py: rank {rank}: {ndev} visible GPU(s) for {local_world} local ranks "
+                     f"(LOCAL_RANK={local})")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo")
+        os.environ.setdefault("MIGMRES_RCCL_INIT_TIMEOUT", str(int(args.comm_timeout)))
+        import datetime
+        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=args.comm_timeout))
+        # every rank alive and through its imports before RCCL's blocking communicator set-up;
+        # monitored_barrier names the rank that did not arrive
+        dist.monitored_barrier(timeout=datetime.timedelta(seconds=args.comm_timeout))
     torch.cuda.set_device(local)
 
     import trilinos_amd as ta
-    from trilinos_amd._lib import call, lib
+    from trilinos_amd._lib import call, lib, rccl_info
     comm = ta.Comm.from_torch_distributed(local) if world > 1 else ta.Comm(local)
 
     nx, k, nb = args.nx, args.k, args.nb
@@ -261,7 +342,11 @@ def main():
     }
     if steps != args.steps:
         out["steps_requested"] = args.steps
-    out["solver_timers_s"] = timers
+    # host-side phases only: the SpMM / ortho / comm phases are asynchronous device work whose
+    # host timers read ~0 unless "Verbosity" synchronises them; their device times are in
+    # "kernels" (HIP events on the library's stream)
+    out["solver_timers_s"] = {key: timers[key] for key in ("total", "lsqr", "setup")}
+    out["rccl"] = rccl_info()
     comm_cls = ("halo", "allreduce")
     if kstats:
         # The metric's "achieved HBM GB/s": the algorithmic bytes the kernels that ran move
@@ -297,7 +382,9 @@ def main():
         out["reference_equivalent"] = {"bytes_per_iteration": model_bytes / steps,
                                        "GBps_per_gpu": model_bytes / elapsed / 1e9 / world}
     if world > 1:
-        mine = {"rank": rank, "comm_host_s": timers.get("comm"),
+        mine = {"rank": rank, "device": local, "rows": A.n_local, "first_row": A.first, "nnz": A.nnz_local,
+                "n_remote": A.n_remote, "n_export": A.n_export,
+                "halo_bytes_per_apply": 8 * k * (A.n_remote + A.n_export),
                 "halo_ms": kstats.get("halo", {}).get("ms"), "halo_launches": kstats.get("halo", {}).get("launches"),
                 "allreduce_ms": kstats.get("allreduce", {}).get("ms"),
                 "allreduce_launches": kstats.get("allreduce", {}).get("launches")}
@@ -306,6 +393,10 @@ def main():
         out["ranks"] = allr
     if rank == 0 and world == 1 and not args.no_cpu_baseline and headline:
         out["cpu_baseline"] = cpu_baseline(k, nb, args.cpu_nx, args.cpu_iters if args.cpu_iters else nb)
+        if not args.no_cpu_one_core:
+            # the baseline also at 1 core -- one whole restart cycle of the
+            # same solver at 128^3 (1/8 of the rows, about 20 s on one core), scaled by rows
+            out["cpu_baseline"]["one_core"] = cpu_baseline_subprocess(1, k, nb, 128, nb)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

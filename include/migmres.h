@@ -64,7 +64,13 @@ const char *migmres_last_error(void);
 
 /* 128-byte RCCL unique id, generated on rank 0 and broadcast by the caller. */
 int migmres_comm_unique_id(unsigned char out[128]);
-/* nranks == 1: uid may be NULL and no communicator is created. */
+/* ncclGetVersion of the RCCL this library is bound to (e.g. 22707 for 2.27.7). */
+int migmres_rccl_version(int *version);
+/* nranks == 1: uid may be NULL and no communicator is created.  For nranks > 1 the
+ * communicator set-up (ncclCommInitRank) is guarded by a watchdog: if it has not returned
+ * after MIGMRES_RCCL_INIT_TIMEOUT seconds (default 600; 0 = no watchdog) -- a peer rank
+ * died or never arrived -- the process prints the reason and exits with status 75, so a
+ * launcher sees a failed rank instead of a hang. */
 int migmres_ctx_create(int device, int rank, int nranks, const unsigned char *uid, migmres_ctx **out);
 int migmres_ctx_destroy(migmres_ctx *ctx);
 int migmres_ctx_sync(migmres_ctx *ctx);

@@ -37,3 +37,34 @@ def test_bench_rejects_mismatched_world(monkeypatch):
         assert "WORLD_SIZE=2" in str(e.code)
     else:
         raise AssertionError("bench.main accepted --gpus 4 with WORLD_SIZE=2")
+
+
+def test_spawn_ranks_stops_blocked_peer_on_failure():
+    # rank 0 waits forever (as in a collective whose peer died); rank 1 fails with 3: the
+    # launcher must return 3 within seconds and leave no rank running
+    import time
+    code = "import os, sys, time; r = os.environ['RANK']; time.sleep(3600) if r == '0' else sys.exit(3)"
+    t0 = time.monotonic()
+    assert bench.spawn_ranks(2, [sys.executable, "-c", code]) == 3
+    assert time.monotonic() - t0 < 20
+
+
+def test_spawn_ranks_timeout_kills_hung_ranks():
+    import time
+    code = "import time; time.sleep(3600)"
+    t0 = time.monotonic()
+    assert bench.spawn_ranks(2, [sys.executable, "-c", code], timeout=2) == 124
+    assert time.monotonic() - t0 < 20
+
+
+def test_bench_rank_refuses_missing_gpus(monkeypatch):
+    # no GPU in this container: a 2-rank job must stop before set_device with a clear message
+    for k, v in dict(WORLD_SIZE="2", RANK="1", LOCAL_RANK="1", LOCAL_WORLD_SIZE="2").items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2", "--deadline", "0"])
+    try:
+        bench.main()
+    except SystemExit as e:
+        assert "visible GPU" in str(e.code)
+    else:
+        raise AssertionError("bench.main ran a 2-rank job without GPUs")

@@ -15,12 +15,12 @@ import pytest
 from oracle import belos as ob, epetra as oe
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SO = os.path.join(ROOT, "oracle", "_ref", "libcport.so")
+SO = os.path.join(ROOT, "oracle", "cport", "libcport.so")
 
 
 def _lib():
     if not os.path.exists(SO):
-        pytest.skip("oracle/_ref/libcport.so not built (make -C oracle/cport)")
+        pytest.skip("oracle/cport/libcport.so not built (make -C oracle/cport)")
     return C.CDLL(SO)
 
 

@@ -1,4 +1,4 @@
-source ./tools_gpu_check.sh
+source ./tools/gpu/step.sh
 export TMPDIR=/tmp
 P=${PROF:-r2i}
 step 400 bench_$P.log python bench.py

@@ -31,6 +31,7 @@ STATUS_FN = C.CFUNCTYPE(i32, vp, i32, i32, P(f64))
 _SIGS = {
     "migmres_abi_version": [],
     "migmres_comm_unique_id": [C.c_char_p],
+    "migmres_rccl_version": [P(i32)],
     "migmres_ctx_create": [i32, i32, i32, C.c_char_p, P(vp)],
     "migmres_ctx_destroy": [vp],
     "migmres_ctx_sync": [vp],
@@ -134,6 +135,25 @@ def call(name, *args):
     if rc != 0:
         raise MigmresError(name, rc)
     return rc
+
+
+def rccl_info():
+    """The RCCL this library is bound to: {"version": "2.27.7", "code": 22707, "library": path}.
+    Which librccl.so the process maps depends on import order (torch bundles its own), so
+    the path is read from /proc/self/maps."""
+    v = i32()
+    call("migmres_rccl_version", C.byref(v))
+    path = None
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                if "librccl" in line:
+                    path = line.split()[-1]
+                    break
+    except OSError:
+        pass
+    c = v.value
+    return {"version": f"{c // 10000}.{c // 100 % 100}.{c % 100}", "code": c, "library": path}
 
 
 def dptr(a):

@@ -10,7 +10,9 @@
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
+#include <cstdio>
 #include <string>
+#include <thread>
 
 using namespace migmres;
 
@@ -320,6 +322,47 @@ extern "C" int migmres_comm_unique_id(unsigned char out[128]) {
   });
 }
 
+extern "C" int migmres_rccl_version(int *version) {
+  return guard([&] {
+    MIG_CHECK(version, "null version pointer");
+    MIG_NCCL(ncclGetVersion(version));
+  });
+}
+
+// ncclCommInitRank blocks until every rank has joined; a rank that died before joining
+// leaves the others there forever.  The watchdog turns that into a process exit (status
+// 75) after MIGMRES_RCCL_INIT_TIMEOUT seconds so the launcher can stop the job.
+static void comm_init_guarded(ncclComm_t *comm, int nranks, const ncclUniqueId &id, int rank) {
+  const char *e = std::getenv("MIGMRES_RCCL_INIT_TIMEOUT");
+  const double limit = e ? std::atof(e) : 600.0;
+  if (limit <= 0) {
+    MIG_NCCL(ncclCommInitRank(comm, nranks, id, rank));
+    return;
+  }
+  std::mutex mu;
+  std::condition_variable cv;
+  bool done = false;
+  std::thread dog([&] {
+    std::unique_lock<std::mutex> lk(mu);
+    if (!cv.wait_for(lk, std::chrono::duration<double>(limit), [&] { return done; })) {
+      std::fprintf(stderr,
+                   "migmres: rank %d of %d: ncclCommInitRank did not complete within %.0f s "
+                   "(a peer rank failed or never joined); exiting\n",
+                   rank, nranks, limit);
+      std::fflush(stderr);
+      std::_Exit(75);
+    }
+  });
+  ncclResult_t r = ncclCommInitRank(comm, nranks, id, rank);
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    done = true;
+  }
+  cv.notify_all();
+  dog.join();
+  if (r != ncclSuccess) throw Error(MIGMRES_ERCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+}
+
 extern "C" int migmres_ctx_create(int device, int rank, int nranks, const unsigned char *uid,
                                   migmres_ctx **out) {
   return guard([&] {
@@ -343,7 +386,7 @@ extern "C" int migmres_ctx_create(int device, int rank, int nranks, const unsign
             MIG_NCCL(ncclGetUniqueId(&id));
           else
             std::memcpy(&id, uid, 128);
-          MIG_NCCL(ncclCommInitRank(&c->comm, nranks, id, rank));
+          comm_init_guarded(&c->comm, nranks, id, rank);
         }
         c->dist = true;
         MIG_HIP(hipStreamCreateWithFlags(&c->halo_stream, hipStreamNonBlocking));

@@ -920,10 +920,15 @@ struct Problem {
     } else {
       // right Jacobi fused into the template SpMM where the operator allows it (one launch,
       // no M x round trip through HBM; same bits); MIGMRES_NO_FUSED_JACOBI=1 disables
+      const auto t0 = Clock::now();
       if (fuse_jacobi && crs_apply_jacobi_fused(*A, *RP, x, y)) {
         ++RP->n_apply;
         ++S->n_prec;
         ++S->n_apply;
+        if (S->p.verbosity & 1) {  // same phase accounting as op()
+          MIG_HIP(hipStreamSynchronize(A->ctx->stream));
+          S->t_spmm += since(t0);
+        }
         return;
       }
       migmres_mv &t = scratch(y.ncols);
