@@ -249,7 +249,8 @@ int migmres_dgks_normalize(migmres_mv *X, double *B, int ldb, int *rank);
  * inverse diagonal as compute() :1240-1270).  A must outlive the preconditioner. */
 int migmres_jacobi_create(migmres_crs *A, int sweeps, double damping, migmres_prec **out);
 int migmres_prec_destroy(migmres_prec *M);
-/* Y = M X (Ifpack2::Relaxation::apply, alpha = 1, beta = 0); X and Y must not alias. */
+/* Y = M X (Ifpack2::Relaxation::apply, alpha = 1, beta = 0).  X may alias Y (apply(x, x)):
+ * the sweeps then read a deep copy of X, as Ifpack2_Relaxation_def.hpp:539-551. */
 int migmres_prec_apply(migmres_prec *M, const migmres_mv *X, migmres_mv *Y);
 /* The stored inverse diagonal (n_local doubles). */
 int migmres_prec_diagonal(const migmres_prec *M, double *dinv_out);

@@ -203,6 +203,72 @@ def brick3d_rows(nx, ny, nz, first, nloc, a=26.0, off=-1.0):
     return _pad_rows(cols, vals)
 
 
+_M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def _mix64(x):
+    """64-bit finaliser (MurmurHash3 fmix64) on uint64 arrays, wrapping arithmetic."""
+    x = np.asarray(x, dtype=np.uint64).copy()
+    with np.errstate(over="ignore"):
+        x ^= x >> np.uint64(33)
+        x *= np.uint64(0xFF51AFD7ED558CCD)
+        x ^= x >> np.uint64(33)
+        x *= np.uint64(0xC4CEB9FE1A85EC53)
+        x ^= x >> np.uint64(33)
+    return x
+
+
+def flan_proxy_rows(nx, ny, nz, first, nloc):
+    """The synthetic stand-in for BASELINE configs[3] (SuiteSparse Flan_1565, not in this
+    image), restated from its SPECIFICATION (include/migmres.h), not from
+    the product's generator: 3 dofs per node of an nx x ny x nz hexahedral node grid (nx odd);
+    node v = (ix, iy, iz) couples to every in-range node u of its 3x3x3 neighbourhood, in
+    dz, dy, dx order from -1 to 1, unless u != v and
+    fmix64(min(u,v) * 0x9e3779b97f4a7c15 + max(u,v)) % 13 == 0 (a symmetric 1/13 of the edges
+    dropped); each coupled node contributes its 3 dofs in order.  Rows and columns are numbered
+    through the scrambled node order p(ix) = (32 ix + 7) mod nx along each grid line (global id
+    3 (p(ix) + nx (iy + ny iz)) + dof).  Off-diagonal value -(h + 1) / 997 with
+    h = fmix64(row * 0x100000001b3 XOR col) % 997; the diagonal (stored in its neighbourhood
+    position) is 1 + the off-diagonal magnitudes summed in insertion order."""
+    assert nx % 2 == 1 and nx > 1 and ny > 0 and nz > 0
+    ainv = pow(32, -1, nx)
+    g = np.arange(first, first + nloc, dtype=np.int64)
+    pv = g // 3
+    nxy = nx * ny
+    iz, iy = pv // nxy, (pv % nxy) // nx
+    ix = ((pv % nx - 7) % nx) * ainv % nx           # undo the scramble
+    v = ix + nx * (iy + ny * iz)
+    cols = np.full((nloc, 81), -1, dtype=np.int64)
+    c = 0
+    for dz in (-1, 0, 1):
+        for dy in (-1, 0, 1):
+            for dx in (-1, 0, 1):
+                jx, jy, jz = ix + dx, iy + dy, iz + dz
+                ok = (jx >= 0) & (jx < nx) & (jy >= 0) & (jy < ny) & (jz >= 0) & (jz < nz)
+                u = jx + nx * (jy + ny * jz)
+                lo = np.minimum(u, v).astype(np.uint64)
+                hi = np.maximum(u, v).astype(np.uint64)
+                with np.errstate(over="ignore"):
+                    key = lo * np.uint64(0x9E3779B97F4A7C15) + hi
+                dropped = (u != v) & (_mix64(key) % np.uint64(13) == 0)
+                ok &= ~dropped
+                pu = ((32 * jx + 7) % nx) + nx * (jy + ny * jz)
+                for e in range(3):
+                    cols[:, c] = np.where(ok, 3 * pu + e, -1)
+                    c += 1
+    with np.errstate(over="ignore"):
+        h = _mix64((g.astype(np.uint64)[:, None] * np.uint64(0x100000001B3)) ^ cols.astype(np.uint64))
+    vals = -((h % np.uint64(997)).astype(np.float64) + 1.0) / 997.0
+    is_diag = cols == g[:, None]
+    vals[is_diag] = 0.0
+    vals[cols < 0] = 0.0
+    off = np.zeros(nloc)
+    for j in range(cols.shape[1]):            # sequential per row, in insertion order
+        off += np.where((cols[:, j] >= 0) & ~is_diag[:, j], -vals[:, j], 0.0)
+    vals = np.where(is_diag, 1.0 + off[:, None], vals)
+    return _pad_rows(cols, vals)
+
+
 # ---------------------------------------------------------------------------
 # Column map and import plan (bit-exact index maps)
 # ---------------------------------------------------------------------------

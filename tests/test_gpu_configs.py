@@ -38,7 +38,6 @@ def comm():
 
 
 def _gen(kind, dims):
-    import trilinos_amd as ta
     from oracle import epetra as oe
     nx, ny, nz = dims
     if kind == "Laplace3D":
@@ -46,7 +45,8 @@ def _gen(kind, dims):
     if kind == "Brick3D":
         return nx * ny * nz, (lambda f, m: oe.brick3d_rows(nx, ny, nz, f, m))
     assert kind == "FlanProxy"
-    return 3 * nx * ny * nz, (lambda f, m: ta.galeri_rows("FlanProxy", nx, ny, nz, f, m))
+    # the oracle's own restatement of the stand-in's specification (not the product generator)
+    return 3 * nx * ny * nz, (lambda f, m: oe.flan_proxy_rows(nx, ny, nz, f, m))
 
 
 def _params(k, nb, **kw):

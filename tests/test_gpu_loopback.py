@@ -110,7 +110,7 @@ def test_distributed_solve_matches_oracle(kind, dims, k, nb, P, env, monkeypatch
         monkeypatch.setenv(key, v)
     import trilinos_amd as ta
     from oracle import belos as ob, epetra as oe
-    from tests.test_gpu_solver import _hist_close, oracle_rerun
+    from tests.parity import hist_close as _hist_close, oracle_rerun
     n, gen = _gen(kind, dims)
     Aor = oe.DistCrs(gen, n, P)
     Xe, _ = oe.epetra_random_mv(5, n, k)
@@ -145,7 +145,7 @@ def test_distributed_solve_matches_oracle(kind, dims, k, nb, P, env, monkeypatch
             assert c["gram_skips"] == c["gram_calls"] > 0
         else:
             assert c["gram_calls"] > 0 and c["gram_skips"] == 0
-        _hist_close(h, ref["history"], rerun)
+        _hist_close(h, ref["history"], rerun, drift_ok=True)
     X = np.zeros((n, k))
     for r in res:
         X[r[4]:r[4] + r[5].shape[0]] = r[5]

@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 
 from tests.test_gpu_loopback import run_ranks
-from tests.test_gpu_solver import _hist_close
+from tests.parity import hist_close as _hist_close, true_residuals_close
 
 pytestmark = pytest.mark.gpu
 
@@ -130,13 +130,13 @@ def _check(res, ref, Aor, B, X, rerun=None):
     assert iters == ref["iterations"]
     assert c["applies"] == ref["n_apply"] and c["prec_applies"] == ref["n_prec"]
     assert c["explicit_checks"] == ref["n_explicit"] and c["restarts"] == ref["restarts"]
-    _hist_close(h, ref["history"], rerun)
+    _hist_close(h, ref["history"], rerun, drift_ok=True)
     dh = float(np.abs(h - ref["history"]).max())
     assert abs(tol - ref["achieved_tol"]) <= max(1e-12, dh)
     # the true residuals of the returned X move with the implicit ones (twice their distance)
     rel = np.linalg.norm(B - Aor.apply(X), axis=0) / np.linalg.norm(B, axis=0)
     rel_ref = np.linalg.norm(B - Aor.apply(ref["X"]), axis=0) / np.linalg.norm(B, axis=0)
-    np.testing.assert_allclose(rel, rel_ref, rtol=1e-3, atol=max(1e-12, 2.0 * dh))
+    true_residuals_close(rel, rel_ref, dh)
 
 
 @pytest.mark.parametrize("case", range(len(CASES)))

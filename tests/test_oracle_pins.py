@@ -173,3 +173,102 @@ def test_reference_run_orsirr1_dgks():
     assert res["converged"] and res["iterations"] == 209
     rel = np.linalg.norm(b - A.apply(res["X"])[:, 0]) / np.linalg.norm(b)
     assert f"{rel:g}" == "9.94786e-06"
+
+
+# ---------------------------------------------------------------------------------------
+# reference unit-test known answers (tests/known_answers.py)
+# ---------------------------------------------------------------------------------------
+
+
+@pytest.mark.parametrize("P", [1, 2, 3])
+def test_ifpack2_relaxation_jacobi_known_answers(P):
+    """Ifpack2_UnitTestRelaxation.cpp Test0 / Test1 on the oracle's Jacobi: applyMat(x = 1)
+    = 2, apply(x = 1) = 0.5, apply(x, x) = 0.5 (5 rows per process, 2 columns)."""
+    from oracle import ifpack2 as oi
+    from tests.known_answers import ifpack2_test_matrix_rows
+    n = 5 * P
+    gen = ifpack2_test_matrix_rows(n)
+    A = oe.DistCrs(gen, n, P)
+    rp, gc, vv = gen(0, n)
+    M = oi.Jacobi(A.apply, oi.crs_diagonal(rp, gc, vv, 0, n))
+    x = np.ones((n, 2))
+    assert np.array_equal(A.apply(x), np.full((n, 2), 2.0))
+    assert np.array_equal(M(x), np.full((n, 2), 0.5))
+    x = M(x)  # apply(x, x): the result replaces x
+    assert np.array_equal(x, np.full((n, 2), 0.5))
+
+
+def _power(gen, n, trans, seed=7):
+    from tests.known_answers import NumpyOps, power_method, transpose_apply
+    A = oe.DistCrs(gen, n, 1)
+    rp, lc, lv = A.crs[0]
+    apply = (lambda q: transpose_apply(rp, lc, lv, q, n)) if trans else A.apply
+    z, _ = oe.epetra_random_mv(seed, n, 1)
+    return power_method(NumpyOps(apply), z, np.zeros((n, 1)), np.zeros((n, 1)))
+
+
+def test_epetra_crsmatrix_power_method_known_answers():
+    """epetra/test/CrsMatrix/cxx_main.cpp:124-317: the (-1, 2, -1) tridiagonal on 10001 rows
+    has 3 n - 2 entries and 2 per end row / 3 per inner row after FillComplete; the power
+    method succeeds (residual < 0.1 within 200 iterations) for A and A^T, with lambda near
+    the largest eigenvalue 2 - 2 cos(pi n / (n + 1)); and again after A[0,0] x 10, where the
+    dominant eigenvalue separates (~20)."""
+    from tests.known_answers import epetra_crs_test_size, epetra_tridiag_rows
+    n = epetra_crs_test_size(1)
+    assert n == 10001
+    gen = epetra_tridiag_rows(n)
+    rp, gc, vv = gen(0, n)
+    assert rp[-1] == 3 * n - 2
+    counts = np.diff(rp)
+    assert counts[0] == counts[-1] == 2 and np.all(counts[1:-1] == 3)
+    lam_max = 2.0 - 2.0 * math.cos(math.pi * n / (n + 1))
+    for trans in (False, True):
+        ierr, lam, lambdas, res = _power(gen, n, trans)
+        assert ierr == 0, res
+        assert 0.99 * lam_max < lam <= lam_max + 1e-12
+    # symmetric A: the transposed product differs only in summation order
+    _, _, l_n, _ = _power(gen, n, False)
+    _, _, l_t, _ = _power(gen, n, True)
+    np.testing.assert_allclose(l_n, l_t, rtol=1e-13)
+    gen10 = epetra_tridiag_rows(n, diag0=20.0)
+    for trans in (False, True):
+        ierr, lam, lambdas, res = _power(gen10, n, trans)
+        assert ierr == 0 and abs(lam - 20.0) < 0.2, (ierr, lam, res)
+    # P > 1 row counts: 10000 P + min(P, 3) global rows, the first three processes one more
+    for P in (2, 3, 4, 5):
+        n = epetra_crs_test_size(P)
+        sizes = [oe.uniform_map(n, P, p)[1] for p in range(P)]
+        assert sizes == [10001 if p < 3 else 10000 for p in range(P)]
+
+
+def _diag_gen(d):
+    d = np.asarray(d, dtype=np.float64)
+
+    def gen(first, m):
+        return np.arange(m + 1, dtype=np.int64), np.arange(first, first + m, dtype=np.int64), d[first:first + m].copy()
+    return gen
+
+
+def test_belos_gmres_diag_known_answers():
+    """belos/epetra/test/BlockGmres/test_bl_gmres_diag.cpp on the oracle's BlockGmresSolMgr
+    (default orthogonalization DGKS): inv(diag(1..10)) 1 = [1, 1/2, ..., 1/10];
+    inv(4 I) 1 = 1/4; the nested inv(inv(4 I) (4 I)) 1 = 1 with ||y - 1|| < 1e-10 -- the
+    inner solve as the outer solve's operator."""
+    from tests.known_answers import DIAG_TEST_PARAMS
+    n = 10
+    x = np.ones((n, 1))
+    D2 = oe.DistCrs(_diag_gen(np.arange(1, n + 1)), n, 1)
+    r = ob.solve(D2.apply, x, DIAG_TEST_PARAMS)
+    assert r["converged"]
+    np.testing.assert_allclose(r["X"][:, 0], 1.0 / np.arange(1, n + 1), rtol=0, atol=1e-10)
+    D = oe.DistCrs(_diag_gen(np.full(n, 4.0)), n, 1)
+
+    def inner(b):
+        return ob.solve(D.apply, b, DIAG_TEST_PARAMS)["X"]
+    y = inner(x)
+    np.testing.assert_allclose(y, 0.25, rtol=0, atol=1e-10)
+
+    def composed(v):  # Composed_Operator(Inner, B): Inner(B v), B = 4 I
+        return inner(4.0 * v)
+    r = ob.solve(composed, x, DIAG_TEST_PARAMS)
+    assert np.linalg.norm(r["X"] - 1.0) < 1e-10

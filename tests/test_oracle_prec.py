@@ -41,11 +41,12 @@ def test_brick3d_structure():
         assert A[g].sum() == 0.0
 
 
-@pytest.mark.parametrize("kind,dims", [("Laplace2D", (9, 7, 1)), ("Laplace3D", (5, 6, 7)), ("Brick3D", (5, 6, 7))])
+@pytest.mark.parametrize("kind,dims", [("Laplace2D", (9, 7, 1)), ("Laplace3D", (5, 6, 7)), ("Brick3D", (5, 6, 7)),
+                                       ("FlanProxy", (9, 8, 7)), ("FlanProxy", (11, 5, 6))])
 def test_native_galeri_rows_match_oracle(kind, dims):
     from trilinos_amd._lib import call
     nx, ny, nz = dims
-    n = nx * ny * (1 if kind == "Laplace2D" else nz)
+    n = nx * ny * (1 if kind == "Laplace2D" else nz) * (3 if kind == "FlanProxy" else 1)
     for first, nloc in [(0, n), (n // 3, n // 2)]:
         nnz = C.c_longlong()
         call("migmres_plan_galeri", kind.encode(), nx, ny, nz, first, nloc, None, None, None, C.byref(nnz))
@@ -57,7 +58,8 @@ def test_native_galeri_rows_match_oracle(kind, dims):
              vv.ctypes.data_as(C.POINTER(C.c_double)), C.byref(nnz))
         gen = {"Laplace2D": lambda f, m: oe.laplace2d_rows(nx, ny, f, m),
                "Laplace3D": lambda f, m: oe.laplace3d_rows(nx, ny, nz, f, m),
-               "Brick3D": lambda f, m: oe.brick3d_rows(nx, ny, nz, f, m)}[kind]
+               "Brick3D": lambda f, m: oe.brick3d_rows(nx, ny, nz, f, m),
+               "FlanProxy": lambda f, m: oe.flan_proxy_rows(nx, ny, nz, f, m)}[kind]
         orp, ogc, ovv = gen(first, nloc)
         assert np.array_equal(rp, orp)
         # same rows; FillComplete sorts, so compare each row's (col, val) set

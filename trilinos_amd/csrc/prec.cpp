@@ -10,6 +10,7 @@ migmres_prec::~migmres_prec() {
   if (d_dinv) hipFree(d_dinv);
   if (d_sdinv) hipFree(d_sdinv);
   delete work;
+  delete xcopy;
 }
 
 namespace migmres {
@@ -17,12 +18,37 @@ namespace migmres {
 // Y = M X.  Zero starting solution: the first sweep is Y = (omega d^-1) X; every further
 // sweep forms R = X - A Y (SpMM with alpha = -1, beta = 1 on a copy of X: y - sum, the
 // Tpetra::Details::residual expression) and Y = 1*Y + (omega d^-1) R.
-void prec_apply(migmres_prec &M, const migmres_mv &X, migmres_mv &Y) {
-  MIG_CHECK(X.ncols == Y.ncols, "Jacobi apply: X and Y column counts differ");
-  MIG_CHECK(X.n_local == M.A->n_local && Y.n_local == M.A->n_local, "Jacobi apply: row map mismatch");
-  MIG_CHECK(X.base != Y.base || X.ncols == 0, "Jacobi apply: X and Y must not alias");
+// Do any columns of X and Y share memory?  (Ifpack2 compares the data pointers,
+// Ifpack2_Relaxation_def.hpp:543-551; a column-range overlap test also catches views that
+// start at different columns of one block.)
+static bool mv_overlap(const migmres_mv &X, const migmres_mv &Y) {
+  if (X.ncols == 0 || Y.ncols == 0 || X.n_local == 0) return false;
+  for (int i = 0; i < X.ncols; ++i) {
+    const double *a0 = X.base + X.col_offset(i), *a1 = a0 + X.n_local;
+    for (int j = 0; j < Y.ncols; ++j) {
+      const double *b0 = Y.base + Y.col_offset(j), *b1 = b0 + Y.n_local;
+      if (a0 < b1 && b0 < a1) return true;
+    }
+  }
+  return false;
+}
+
+void prec_apply(migmres_prec &M, const migmres_mv &X_in, migmres_mv &Y) {
+  MIG_CHECK(X_in.ncols == Y.ncols, "Jacobi apply: X and Y column counts differ");
+  MIG_CHECK(X_in.n_local == M.A->n_local && Y.n_local == M.A->n_local, "Jacobi apply: row map mismatch");
   migmres_ctx *c = M.ctx;
   const int n = M.A->n_local;
+  // X aliasing Y (apply(x, x)): sweep from a deep copy of X, as the reference does
+  const migmres_mv *Xp = &X_in;
+  if (mv_overlap(X_in, Y)) {
+    if (!M.xcopy || M.xcopy->ncols != X_in.ncols) {
+      delete M.xcopy;
+      M.xcopy = mv_create(c, X_in.n_global, X_in.n_local, X_in.ncols);
+    }
+    mv_assign(X_in, *M.xcopy);
+    Xp = M.xcopy;
+  }
+  const migmres_mv &X = *Xp;
   {
     ProfScope ps(c, K_AXPBY, 8.0 * n * (2.0 * X.ncols + 1.0));
     launch_jacobi(c->stream, X.desc(), Y.desc(), M.d_dinv, M.damping, n, false);

@@ -181,7 +181,8 @@ struct migmres_prec {
   int sweeps = 1;
   double damping = 1.0;
   long long n_apply = 0;
-  migmres_mv *work = nullptr;  // residual scratch for sweeps > 1
+  migmres_mv *work = nullptr;   // residual scratch for sweeps > 1
+  migmres_mv *xcopy = nullptr;  // deep copy of X when apply(X, Y) aliases
   ~migmres_prec();
 };
 

@@ -67,11 +67,29 @@ class Relaxation:
     def isComputed(self):
         return self.h is not None
 
-    def apply(self, X, Y):
-        """Y = M X (alpha = 1, beta = 0)."""
+    def apply(self, X, Y, alpha=1.0, beta=0.0):
+        """Y = alpha M X (Ifpack2_Relaxation_def.hpp:494-592): beta != 0 is rejected as in the
+        reference, alpha == 0 zeroes Y, X may be Y (the sweeps then read a copy of X)."""
         if self.h is None:
             raise RuntimeError("Ifpack2::Relaxation::apply: compute() has not been called")
+        if X.ncols != Y.ncols:
+            raise RuntimeError("Ifpack2::Relaxation::apply: X and Y have different numbers of columns")
+        if beta != 0.0:
+            raise NotImplementedError(f"Ifpack2::Relaxation::apply: beta = {beta} != 0 case not implemented")
+        if alpha == 0.0:
+            Y.put_scalar(0.0)
+            return
         call("migmres_prec_apply", self.h, X.h, Y.h)
+        if alpha != 1.0:
+            call("migmres_mv_scale", Y.h, float(alpha))
+
+    def applyMat(self, X, Y):
+        """Y = A X with the preconditioner's matrix (Ifpack2_Relaxation_def.hpp:596-615)."""
+        if self.h is None:
+            raise RuntimeError("Ifpack2::Relaxation::applyMat: compute() has not been called")
+        if X.ncols != Y.ncols:
+            raise ValueError("Ifpack2::Relaxation::applyMat: X and Y have different numbers of columns")
+        self.A.apply(X, Y)
 
     def inverseDiagonal(self):
         out = np.zeros(self.A.n_local)
