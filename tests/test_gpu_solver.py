@@ -60,6 +60,9 @@ def _device_solve(comm, kind, dims, k, seed, params, nrhs=None):
     return sm, ret, X.download(), B.download(), Xex
 
 
+# The 16^3 k = 8 case restarts 6 times and is named restart-sensitive: measured on MI355X
+# 1.6e-12 from the oracle against an oracle-vs-oracle drift of 8.2e-13
+# (profiles/r3_parity_margins.jsonl); the other cases meet the strict 1e-12 bar.
 @pytest.mark.parametrize("kind,dims,k,nb,seed", [("Laplace2D", (30, 30, 1), 1, 20, 1),
                                                  ("Laplace2D", (40, 25, 1), 3, 20, 2),
                                                  ("Laplace3D", (16, 16, 16), 8, 6, 3),
@@ -79,7 +82,8 @@ def test_small_solves_match_oracle(comm, kind, dims, k, nb, seed):
     assert c["explicit_checks"] == ref["n_explicit"]
     assert c["restarts"] == ref["restarts"]
     assert c["applies"] == ref["n_apply"]
-    _hist_close(sm.residualHistory(), ref["history"], oracle_rerun(ob.solve, Aor.apply, Aor.apply(Xex), params), drift_ok=True)
+    _hist_close(sm.residualHistory(), ref["history"], oracle_rerun(ob.solve, Aor.apply, Aor.apply(Xex), params),
+                drift_ok=(kind, dims) == ("Laplace3D", (16, 16, 16)))
     rel = np.linalg.norm(B - Aor.apply(X), axis=0) / np.linalg.norm(B, axis=0)
     assert rel.max() <= 1e-9
 
@@ -121,7 +125,7 @@ def test_multiple_rhs_blocks(comm):
         ref = ob.solve(Aor.apply, Aor.apply(Xex), params)
         assert sm.getNumIters() == ref["iterations"]
         assert sm.counters()["applies"] == ref["n_apply"]
-        _hist_close(sm.residualHistory(), ref["history"], oracle_rerun(ob.solve, Aor.apply, Aor.apply(Xex), params), drift_ok=True)
+        _hist_close(sm.residualHistory(), ref["history"], oracle_rerun(ob.solve, Aor.apply, Aor.apply(Xex), params))
         assert ret == ta.Converged
         rel = np.linalg.norm(B - Aor.apply(X), axis=0) / np.linalg.norm(B, axis=0)
         assert rel.max() <= 1e-8
@@ -169,7 +173,7 @@ def test_reference_pinned_runs(comm, name):
     c = sm.counters()
     assert c["applies"] == meta["n_apply"] and c["explicit_checks"] == meta["n_explicit"]
     assert c["restarts"] == meta["restarts"]
-    _hist_close(sm.residualHistory(), gold["history"], gold["history_reversed"], drift_ok=True)
+    _hist_close(sm.residualHistory(), gold["history"], gold["history_reversed"])
     from oracle import epetra as oe
     n, gen = _gen(meta["kind"], tuple(meta["dims"]))
     rel = np.linalg.norm(B - oe.DistCrs(gen, n, 1).apply(X), axis=0) / np.linalg.norm(B, axis=0)
@@ -239,7 +243,7 @@ def test_dgks_solves_match_oracle(comm, kind, dims, k, nb, seed):
     assert sm.getNumIters() == ref["iterations"]
     assert c["restarts"] == ref["restarts"] and c["applies"] == ref["n_apply"]
     assert c["explicit_checks"] == ref["n_explicit"]
-    _hist_close(sm.residualHistory(), ref["history"], oracle_rerun(ob.solve, A.apply, A.apply(Xex), params), drift_ok=True)
+    _hist_close(sm.residualHistory(), ref["history"], oracle_rerun(ob.solve, A.apply, A.apply(Xex), params))
 
 
 def test_dgks_orsirr1_reference_run(comm):
@@ -267,25 +271,28 @@ def test_dgks_orsirr1_reference_run(comm):
     assert f"{rel:.5e}" == "9.94786e-06"
     ref = ob.solve(Aor.apply, b[:, None], dict(params, Orthogonalization="DGKS"))
     _hist_close(sm.residualHistory(), ref["history"],
-                oracle_rerun(ob.solve, Aor.apply, b[:, None], dict(params, Orthogonalization="DGKS")), drift_ok=True)
+                oracle_rerun(ob.solve, Aor.apply, b[:, None], dict(params, Orthogonalization="DGKS")))
 
 
 GRAM_KEYS = ("gram_calls", "gram_skips")
 
 
+@pytest.mark.parametrize("ortho", ["ICGS", "DGKS"])
 @pytest.mark.parametrize("k", [4, 12, 16])
 @pytest.mark.parametrize("env", [{"MIGMRES_FB_GRAM": "0"}, {"MIGMRES_FB_GRAM_GATE": "2"},
                                  {"MIGMRES_FB_GRAM_FUSE": "0"}])
-def test_gram_findbasis_against_column_passes(comm, monkeypatch, env, k):
+def test_gram_findbasis_against_column_passes(comm, monkeypatch, env, k, ortho):
     """findBasis in Gram form (CholQR2 of the block with the reference's dependency tests on
     its pivots; the default for ICGS with 2 <= k <= 16: k <= 8 with G1 taken by the closing
     update, k > 8 by the MFMA Gram kernels) against the column-by-column passes
     (MIGMRES_FB_GRAM=0), against its own gate hand-back (gate 2: every block goes to the
     column passes, after the speculative SpMM has read it) and against its unfused form: the
     same solver decisions and iteration counts, histories within the oracle bar.  The Gram
-    counters show which path ran (a gram_ok regression must not pass silently)."""
+    counters show which path ran (a gram_ok regression must not pass silently).
+    DGKS (the Belos default) takes the same Gram form for k > 1; against its column passes,
+    which re-orthogonalise a column only when it lost more than 1 - 1/sqrt(2) of its norm."""
     params = {"Block Size": k, "Num Blocks": 10, "Maximum Iterations": 400, "Maximum Restarts": 40,
-              "Convergence Tolerance": 1e-9, "Orthogonalization": "ICGS"}
+              "Convergence Tolerance": 1e-9, "Orthogonalization": ortho}
     sm, ret, X, _, _ = _device_solve(comm, "Laplace3D", (14, 13, 12), k, 7, params)
     c = sm.counters()
     assert c["gram_calls"] > 0 and c["gram_skips"] == 0, c
@@ -311,7 +318,7 @@ def test_gram_findbasis_against_column_passes(comm, monkeypatch, env, k):
         h1 = ob.solve(Aor.apply, B, params)["history"]
         # the first GPU history shifted by the oracle's summation-order drift
         return sm.residualHistory() + (oracle_rerun(ob.solve, Aor.apply, B, params)() - h1)
-    _hist_close(sm2.residualHistory(), sm.residualHistory(), drift, drift_ok=True)
+    _hist_close(sm2.residualHistory(), sm.residualHistory(), drift, drift_ok=k == 12)
     np.testing.assert_allclose(X2, X, rtol=0, atol=1e-8 * np.abs(X).max())
 
 
@@ -362,6 +369,6 @@ def test_one_rank_rccl_transport(monkeypatch):
     assert rccl[1] == plain[1] == ref["iterations"]
     for key in ("applies", "restarts", "explicit_checks"):
         assert rccl[2][key] == plain[2][key]
-    _hist_close(rccl[3], ref["history"], oracle_rerun(ob.solve, Aor.apply, Bh, params), drift_ok=True)
+    _hist_close(rccl[3], ref["history"], oracle_rerun(ob.solve, Aor.apply, Bh, params))
     np.testing.assert_allclose(rccl[4], plain[4], rtol=0, atol=1e-12 * np.abs(plain[4]).max())
     assert np.array_equal(rccl[5], [1.5, -2.0])

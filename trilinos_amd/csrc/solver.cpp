@@ -584,10 +584,19 @@ struct FastIcgs {
 
   bool gram_ok(int L, int k) const {
     // k <= 8: the closing update carries G1's partials (its LDS holds L x k coefficients);
-    // 9 <= k <= 16: plain closing update, then G1 in a pass of its own (MFMA Gram kernels)
-    return gram_on && !slow->dgks && slow->steps == 2 && k >= 2 && L >= 1 && L <= 1024 &&
+    // 9 <= k <= 16: plain closing update, then G1 in a pass of its own (MFMA Gram kernels).
+    // DGKS (the Belos default) shares it: for k > 1 its blkOrtho is ICGS's (both passes,
+    // BelosDGKSOrthoManager.hpp:1373-1492) and its findBasis differs only in skipping the
+    // second projection of a column that kept >= dep_tol of its norm (:1094-1119), i.e. in
+    // rounding, with the same dependency test newDot < blk_tol oldDot (:1204-1210) that the
+    // Gram form takes on its pivots.  MIGMRES_FB_GRAM_DGKS=0 keeps DGKS on the column passes.
+    return gram_on && (!slow->dgks || gram_dgks) && slow->steps == 2 && k >= 2 && L >= 1 && L <= 1024 &&
            ((k <= 8 && L * k <= 7680) || (k > 8 && k <= 16));
   }
+  bool gram_dgks = [] {
+    const char *e = std::getenv("MIGMRES_FB_GRAM_DGKS");
+    return !(e && e[0] == '0');
+  }();
   void gram_alloc() {
     if (gb.part) return;
     MIG_HIP(hipMalloc(&gb.part, sizeof(double) * 1024 * 136));
