@@ -67,21 +67,31 @@ struct MvDesc {
 // Y[:,c] = alpha * (A X)[:,c] + beta * Y[:,c] for the local CSR rows.  Column ids
 // >= n_local index the ghost block (column-major, leading dim ldg).  Row sums are
 // accumulated in stored order without contraction (Epetra GeneralMM order).
+// Column scale of the fused right Jacobi preconditioner: the operand of every entry is
+// (omega d^-1)_col * x_col, formed exactly as k_jacobi forms (omega D^-1) X.  own: n_local
+// (+2 zero) entries; ghost: the owners' values of the ghost columns (ldg + 2 entries, zero
+// padded), imported once.  Both null: no scaling.
+struct ColScale {
+  const double *own = nullptr;
+  const double *ghost = nullptr;
+};
 // Row-pair SpMM (plan from make_pair_plan); vals padded by 8 entries, ghost ld even.
 // sel/nsel: optional subset of pairs (rows for launch_spmm) to compute -- the interior and
 // boundary halves of the halo overlap.
 void launch_spmm_pair(hipStream_t s, int n_local, int max_keys, int rmax, const double *sv, const int *sk,
                       const unsigned short *sm, MvDesc X, const double *ghost, long long ldg, MvDesc Y,
-                      double alpha, double beta, const int *sel = nullptr, int nsel = 0);
+                      double alpha, double beta, const int *sel = nullptr, int nsel = 0, ColScale cs = {});
 // General rows: thread per row over the SELL-64 copy (make_sell64); sel lists rows.
 // xr (optional, n_local x 8 doubles): scratch for a row-interleaved copy of X's owned rows,
-// so each entry's k operands are one contiguous segment instead of k column gathers.
+// so each entry's k operands are one contiguous segment instead of k column gathers;
+// xr_ready: an earlier launch of this apply already filled it (k <= 8).
 void launch_spmm_sell(hipStream_t s, int n_local, const long long *off, const int *len, const int *scol,
                       const double *sval, MvDesc X, const double *ghost, long long ldg, MvDesc Y, double alpha,
-                      double beta, const int *sel = nullptr, int nsel = 0, double *xr = nullptr);
+                      double beta, const int *sel = nullptr, int nsel = 0, double *xr = nullptr,
+                      bool xr_ready = false, ColScale cs = {});
 void launch_spmm(hipStream_t s, int row_begin, int row_end, const int *rowptr, const int *cols,
                  const double *vals, MvDesc X, int n_local, const double *ghost, long long ldg,
-                 MvDesc Y, double alpha, double beta, const int *sel = nullptr, int nsel = 0);
+                 MvDesc Y, double alpha, double beta, const int *sel = nullptr, int nsel = 0, ColScale cs = {});
 // Row-pair templates (make_pair_templates): every pair whose template id is not kTplNone;
 // the others are left to one of the kernels above.
 // colscale (optional): Y = alpha A diag(colscale) X + beta Y with diag(colscale) X formed per

@@ -42,7 +42,8 @@ __global__ __launch_bounds__(256) void k_spmm(int row_begin, int row_end,
                                               int n_local, const double *__restrict__ ghost,
                                               long long ldg, MvDesc Y, int c0, int kc,
                                               double alpha, double beta, const int *__restrict__ sel,
-                                              int nsel) {
+                                              int nsel, const double *__restrict__ cs,
+                                              const double *__restrict__ gcs) {
 #pragma clang fp contract(off)
   int r = row_begin + blockIdx.x * 256 + threadIdx.x;
   if (sel) {  // optional list of rows (interior / boundary split of the halo overlap)
@@ -83,10 +84,14 @@ __global__ __launch_bounds__(256) void k_spmm(int row_begin, int row_end,
       const int col = ci[j];
       const bool own = col < n_local;
       const int g = col - n_local;
+      // fused right Jacobi: the operand (omega D^-1) x as k_jacobi forms it (ghost columns
+      // scaled by their owner's omega d^-1, imported once)
+      const double sc = cs ? (own ? cs[col] : gcs[g]) : 1.0;
 #pragma unroll
       for (int c = 0; c < KC; ++c) {
         if (c < kc) {
-          const double x = own ? xc[c][col] : gc[c][g];
+          double x = own ? xc[c][col] : gc[c][g];
+          if (cs) x = sc * x;
           const double prod = v[j] * x;
           sum[c] = sum[c] + (ok ? prod : 0.0);
         }
@@ -107,7 +112,7 @@ __global__ __launch_bounds__(256) void k_spmm(int row_begin, int row_end,
 
 void launch_spmm(hipStream_t s, int row_begin, int row_end, const int *rowptr, const int *cols,
                  const double *vals, MvDesc X, int n_local, const double *ghost, long long ldg,
-                 MvDesc Y, double alpha, double beta, const int *sel, int nsel) {
+                 MvDesc Y, double alpha, double beta, const int *sel, int nsel, ColScale cs) {
   const int n = sel ? nsel : row_end - row_begin;
   if (n <= 0) return;
   const int k = Y.ncols;
@@ -115,15 +120,15 @@ void launch_spmm(hipStream_t s, int row_begin, int row_end, const int *rowptr, c
   for (int c0 = 0; c0 < k; c0 += 16) {
     const int kc = (k - c0) < 16 ? (k - c0) : 16;
     if (kc == 1)
-      k_spmm<1><<<grid, 256, 0, s>>>(row_begin, row_end, rowptr, cols, vals, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel);
+      k_spmm<1><<<grid, 256, 0, s>>>(row_begin, row_end, rowptr, cols, vals, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel, cs.own, cs.ghost);
     else if (kc <= 2)
-      k_spmm<2><<<grid, 256, 0, s>>>(row_begin, row_end, rowptr, cols, vals, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel);
+      k_spmm<2><<<grid, 256, 0, s>>>(row_begin, row_end, rowptr, cols, vals, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel, cs.own, cs.ghost);
     else if (kc <= 4)
-      k_spmm<4><<<grid, 256, 0, s>>>(row_begin, row_end, rowptr, cols, vals, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel);
+      k_spmm<4><<<grid, 256, 0, s>>>(row_begin, row_end, rowptr, cols, vals, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel, cs.own, cs.ghost);
     else if (kc <= 8)
-      k_spmm<8><<<grid, 256, 0, s>>>(row_begin, row_end, rowptr, cols, vals, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel);
+      k_spmm<8><<<grid, 256, 0, s>>>(row_begin, row_end, rowptr, cols, vals, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel, cs.own, cs.ghost);
     else
-      k_spmm<16><<<grid, 256, 0, s>>>(row_begin, row_end, rowptr, cols, vals, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel);
+      k_spmm<16><<<grid, 256, 0, s>>>(row_begin, row_end, rowptr, cols, vals, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel, cs.own, cs.ghost);
     LAUNCH_CHECK();
   }
 }
@@ -144,7 +149,8 @@ __global__ __launch_bounds__(256) void k_spmm_sell(int n, const long long *__res
                                                    const double *__restrict__ ghost, long long ldg, MvDesc Y,
                                                    int c0, int kc, double alpha, double beta,
                                                    const int *__restrict__ sel, int nsel,
-                                                   const double *__restrict__ xr = nullptr) {
+                                                   const double *__restrict__ xr, const double *__restrict__ cs,
+                                                   const double *__restrict__ gcs) {
 #pragma clang fp contract(off)
   // entries whose KC x loads are issued together (XR: KC / 2 16-byte loads per entry; 8
   // entries at a time there measured the same as 4 on FlanProxy)
@@ -184,10 +190,13 @@ __global__ __launch_bounds__(256) void k_spmm_sell(int n, const long long *__res
 #pragma unroll
     for (int j0 = 0; j0 < 8; j0 += J) {
       double xv[J][KC];
+      double sc[J];
 #pragma unroll
       for (int j = 0; j < J; ++j) {
         const int col = ci[j0 + j];
         const bool own = col < n_local;
+        // fused right Jacobi: (omega d^-1) of the column (owner's value for a ghost column)
+        sc[j] = cs ? (own ? cs[col] : gcs[col - n_local]) : 1.0;
         if constexpr (XR) {
           if (own) {
             const d2 *xp = (const d2 *)(xr + (long long)col * KC);
@@ -212,7 +221,8 @@ __global__ __launch_bounds__(256) void k_spmm_sell(int n, const long long *__res
         const bool ok = sb + j0 + j < L;
 #pragma unroll
         for (int c = 0; c < KC; ++c) {
-          const double prod = v[j0 + j] * xv[j][c];
+          const double x = cs ? sc[j] * xv[j][c] : xv[j][c];
+          const double prod = v[j0 + j] * x;
           sum[c] = sum[c] + (ok ? prod : 0.0);
         }
       }
@@ -245,7 +255,7 @@ __global__ __launch_bounds__(256) void k_interleave(MvDesc X, int c0, int kc, in
 
 void launch_spmm_sell(hipStream_t s, int n_local, const long long *off, const int *len, const int *scol,
                       const double *sval, MvDesc X, const double *ghost, long long ldg, MvDesc Y, double alpha,
-                      double beta, const int *sel, int nsel, double *xr) {
+                      double beta, const int *sel, int nsel, double *xr, bool xr_ready, ColScale cs) {
   const int n = sel ? nsel : n_local;
   if (n <= 0) return;
   const int k = Y.ncols;
@@ -254,10 +264,13 @@ void launch_spmm_sell(hipStream_t s, int n_local, const long long *off, const in
     const int kc = (k - c0) < 8 ? (k - c0) : 8;
     if (xr && kc >= 2) {
       const dim3 gi(cdiv(n_local, 256));
+      // xr_ready: an earlier launch of the same apply (interior rows) already interleaved X;
+      // only with one column chunk, since xr holds one chunk at a time
+      const bool fresh = !(xr_ready && k <= 8);
 #define SELL_XR(KC)                                                                                            \
-  k_interleave<KC><<<gi, 256, 0, s>>>(X, c0, kc, n_local, xr);                                               \
+  if (fresh) k_interleave<KC><<<gi, 256, 0, s>>>(X, c0, kc, n_local, xr);                                    \
   k_spmm_sell<KC, true><<<grid, 256, 0, s>>>(n_local, off, len, scol, sval, X, n_local, ghost, ldg, Y, c0, kc, \
-                                             alpha, beta, sel, nsel, xr);
+                                             alpha, beta, sel, nsel, xr, cs.own, cs.ghost);
       if (kc <= 2) {
         SELL_XR(2)
       } else if (kc <= 4) {
@@ -270,13 +283,13 @@ void launch_spmm_sell(hipStream_t s, int n_local, const long long *off, const in
       continue;
     }
     if (kc == 1)
-      k_spmm_sell<1><<<grid, 256, 0, s>>>(n_local, off, len, scol, sval, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel);
+      k_spmm_sell<1><<<grid, 256, 0, s>>>(n_local, off, len, scol, sval, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel, nullptr, cs.own, cs.ghost);
     else if (kc <= 2)
-      k_spmm_sell<2><<<grid, 256, 0, s>>>(n_local, off, len, scol, sval, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel);
+      k_spmm_sell<2><<<grid, 256, 0, s>>>(n_local, off, len, scol, sval, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel, nullptr, cs.own, cs.ghost);
     else if (kc <= 4)
-      k_spmm_sell<4><<<grid, 256, 0, s>>>(n_local, off, len, scol, sval, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel);
+      k_spmm_sell<4><<<grid, 256, 0, s>>>(n_local, off, len, scol, sval, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel, nullptr, cs.own, cs.ghost);
     else
-      k_spmm_sell<8><<<grid, 256, 0, s>>>(n_local, off, len, scol, sval, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel);
+      k_spmm_sell<8><<<grid, 256, 0, s>>>(n_local, off, len, scol, sval, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel, nullptr, cs.own, cs.ghost);
     LAUNCH_CHECK();
   }
 }
@@ -298,7 +311,8 @@ __global__ __launch_bounds__(256) void k_spmm_pair(int npairs, int rmax, const d
                                                    const unsigned short *__restrict__ sm, MvDesc X, int n_local,
                                                    const double *__restrict__ ghost, long long ldg, MvDesc Y,
                                                    int c0, int kc, double alpha, double beta,
-                                                   const int *__restrict__ sel, int nsel) {
+                                                   const int *__restrict__ sel, int nsel,
+                                                   const double *__restrict__ cs, const double *__restrict__ gcs) {
 #pragma clang fp contract(off)
   // sel: optional list of the pairs to compute (interior / boundary split of the halo overlap)
   int p = blockIdx.x * 256 + threadIdx.x;
@@ -344,6 +358,14 @@ __global__ __launch_bounds__(256) void k_spmm_pair(int npairs, int rmax, const d
       use |= (used ? 1ull : 0ull) << (4 * u + sl);
     }
   }
+  // fused right Jacobi: per key the (omega d^-1) pair of its two columns (the owner's values
+  // for ghost columns, imported once); zero padding past the last row / ghost
+  d2 sc[PAIR_MAXK];
+  if (cs) {
+#pragma unroll
+    for (int u = 0; u < PAIR_MAXK; ++u)
+      sc[u] = *(const d2 *)(key[u] >= 0 ? cs + 2LL * key[u] : gcs + 2LL * (-key[u] - 1));
+  }
 #pragma unroll
   for (int c = 0; c < KC; ++c) {
     if (c >= kc) break;
@@ -354,7 +376,8 @@ __global__ __launch_bounds__(256) void k_spmm_pair(int npairs, int rmax, const d
     for (int u = 0; u < PAIR_MAXK; ++u) {
       const int kk = key[u];
       const double *src = kk >= 0 ? xc + 2LL * kk : gc + 2LL * (-kk - 1);
-      const d2 x = *(const d2 *)src;
+      d2 x = *(const d2 *)src;
+      if (cs) x = sc[u] * x;
       const double pa0 = cx[u][0] * x.x, pa1 = cx[u][1] * x.y;
       const double pb0 = cx[u][2] * x.x, pb1 = cx[u][3] * x.y;
       sa = sa + ((use >> (4 * u)) & 1ull ? pa0 : 0.0);
@@ -382,7 +405,7 @@ __global__ __launch_bounds__(256) void k_spmm_pair(int npairs, int rmax, const d
 template <int MAXK>
 static void spmm_pair_cols(hipStream_t s, int npairs, int rmax, const double *sv, const int *sk,
                            const unsigned short *sm, MvDesc X, int n_local, const double *ghost, long long ldg,
-                           MvDesc Y, double alpha, double beta, const int *sel, int nsel) {
+                           MvDesc Y, double alpha, double beta, const int *sel, int nsel, ColScale cs) {
   const int k = Y.ncols;
   const int units = sel ? nsel : npairs;
   if (units <= 0) return;
@@ -390,27 +413,27 @@ static void spmm_pair_cols(hipStream_t s, int npairs, int rmax, const double *sv
   for (int c0 = 0; c0 < k; c0 += 8) {
     const int kc = (k - c0) < 8 ? (k - c0) : 8;
     if (kc == 1)
-      k_spmm_pair<1, MAXK><<<grid, 256, 0, s>>>(npairs, rmax, sv, sk, sm, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel);
+      k_spmm_pair<1, MAXK><<<grid, 256, 0, s>>>(npairs, rmax, sv, sk, sm, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel, cs.own, cs.ghost);
     else if (kc <= 2)
-      k_spmm_pair<2, MAXK><<<grid, 256, 0, s>>>(npairs, rmax, sv, sk, sm, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel);
+      k_spmm_pair<2, MAXK><<<grid, 256, 0, s>>>(npairs, rmax, sv, sk, sm, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel, cs.own, cs.ghost);
     else if (kc <= 4)
-      k_spmm_pair<4, MAXK><<<grid, 256, 0, s>>>(npairs, rmax, sv, sk, sm, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel);
+      k_spmm_pair<4, MAXK><<<grid, 256, 0, s>>>(npairs, rmax, sv, sk, sm, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel, cs.own, cs.ghost);
     else
-      k_spmm_pair<8, MAXK><<<grid, 256, 0, s>>>(npairs, rmax, sv, sk, sm, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel);
+      k_spmm_pair<8, MAXK><<<grid, 256, 0, s>>>(npairs, rmax, sv, sk, sm, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel, cs.own, cs.ghost);
     LAUNCH_CHECK();
   }
 }
 
 void launch_spmm_pair(hipStream_t s, int n_local, int max_keys, int rmax, const double *sv, const int *sk,
                       const unsigned short *sm, MvDesc X, const double *ghost, long long ldg, MvDesc Y,
-                      double alpha, double beta, const int *sel, int nsel) {
+                      double alpha, double beta, const int *sel, int nsel, ColScale cs) {
   const int npairs = (n_local + 1) / 2;
   if (npairs <= 0) return;
   if (rmax > PAIR_MAXR) throw Error(MIGMRES_EINVAL, "spmm_pair: rows longer than 8 entries");
   // instantiated for the exact key count (the SELL plan is laid out with that stride)
 #define PAIR_CASE(K) \
   case K:            \
-    spmm_pair_cols<K>(s, npairs, rmax, sv, sk, sm, X, n_local, ghost, ldg, Y, alpha, beta, sel, nsel); \
+    spmm_pair_cols<K>(s, npairs, rmax, sv, sk, sm, X, n_local, ghost, ldg, Y, alpha, beta, sel, nsel, cs); \
     break;
   switch (max_keys) {
     PAIR_CASE(1)

@@ -9,6 +9,7 @@ using namespace migmres;
 migmres_prec::~migmres_prec() {
   if (d_dinv) hipFree(d_dinv);
   if (d_sdinv) hipFree(d_sdinv);
+  if (d_gsdinv) hipFree(d_gsdinv);
   delete work;
   delete xcopy;
 }
@@ -88,6 +89,7 @@ extern "C" int migmres_jacobi_create(migmres_crs *A, int sweeps, double damping,
     MIG_HIP(hipMemsetAsync(M->d_sdinv, 0, sizeof(double) * ((size_t)n + 2), A->ctx->stream));
     launch_scaled_copy(A->ctx->stream, M->d_dinv, damping, M->d_sdinv, n);
     MIG_HIP(hipStreamSynchronize(A->ctx->stream));
+    if (sweeps == 1) prec_import_ghost_scale(*M);  // the fused form's ghost column scale
     *out = M;
   });
 }

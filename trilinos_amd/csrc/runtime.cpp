@@ -975,7 +975,9 @@ static void crs_finish(migmres_crs *A, const long long *rowptr, std::vector<int>
   }
 }
 
-void crs_apply(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, double alpha, double beta) {
+// Y = alpha A diag(cs) X + beta Y (cs: the fused right Jacobi's column scale, or none).
+static void crs_apply_impl(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, double alpha, double beta,
+                           ColScale cs) {
   MIG_CHECK(X.n_local == A.n_local && Y.n_local == A.n_local, "apply: row maps differ");
   MIG_CHECK(X.ncols == Y.ncols, "apply: column counts differ");
   migmres_ctx *c = A.ctx;
@@ -998,16 +1000,19 @@ void crs_apply(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, double alpha,
     if (!A.d_xr) MIG_HIP(hipMalloc(&A.d_xr, sizeof(double) * 8 * (size_t)A.n_local));
     xr = A.d_xr;
   }
+  bool xr_ready = false;  // the interleaved X copy is made once per apply (interior launch)
   auto spmm = [&](const int *sel, int nsel) {
-    if (A.use_pairs)
+    if (A.use_pairs) {
       launch_spmm_pair(c->stream, A.n_local, A.pair_max_keys, A.pair_rmax, A.d_psv, A.d_psk, A.d_psm, X.desc(),
-                       A.d_ghost, A.ldg, Y.desc(), alpha, beta, sel, nsel);
-    else if (A.use_sell)
+                       A.d_ghost, A.ldg, Y.desc(), alpha, beta, sel, nsel, cs);
+    } else if (A.use_sell) {
       launch_spmm_sell(c->stream, A.n_local, A.d_soff, A.d_slen, A.d_scol, A.d_sval, X.desc(), A.d_ghost, A.ldg,
-                       Y.desc(), alpha, beta, sel, nsel, xr);
-    else
+                       Y.desc(), alpha, beta, sel, nsel, xr, xr_ready, cs);
+      xr_ready = xr != nullptr;
+    } else {
       launch_spmm(c->stream, 0, A.n_local, A.d_rowptr, A.d_cols, A.d_vals, X.desc(), A.n_local, A.d_ghost, A.ldg,
-                  Y.desc(), alpha, beta, sel, nsel);
+                  Y.desc(), alpha, beta, sel, nsel, cs);
+    }
   };
   if (halo) {
     if (k > A.halo_k) {
@@ -1044,12 +1049,13 @@ void crs_apply(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, double alpha,
     MIG_HIP(hipEventRecord(c->ev_halo, c->halo_stream));
     c->comm_seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
-  ProfScope ps(c, K_SPMM, A.spmm_fixed_bytes + 8.0 * A.n_local * k * (beta == 0.0 ? 2.0 : 3.0));
+  ProfScope ps(c, K_SPMM, A.spmm_fixed_bytes + 8.0 * A.n_local * k * (beta == 0.0 ? 2.0 : 3.0) +
+                            (cs.own ? 8.0 * A.n_local : 0.0));
   if (A.use_tpl) {
     // templated pairs read no ghost column: they run while the halo is in flight, then the
     // pairs that do read one go to the fallback kernel
     launch_spmm_tpl(c->stream, A.n_local, A.d_tpl_id, A.d_tpl_rec, A.tpl_ntpl, A.tpl_maxk, A.d_tpl_val,
-                    A.tpl_nvals, X.desc(), Y.desc(), alpha, beta);
+                    A.tpl_nvals, X.desc(), Y.desc(), alpha, beta, cs.own);
     if (halo) MIG_HIP(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
     if (A.n_tpl_rest > 0) spmm(A.d_tpl_rest, A.n_tpl_rest);
   } else if (halo && A.d_sel_int) {
@@ -1063,18 +1069,53 @@ void crs_apply(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, double alpha,
   }
 }
 
+void crs_apply(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, double alpha, double beta) {
+  crs_apply_impl(A, X, Y, alpha, beta, ColScale{});
+}
+
+// Y = A (M X) for the one-sweep right Jacobi M = omega D^-1 in one SpMM: every kernel forms
+// the operand (omega d^-1)_col x_col in registers, exactly as k_jacobi forms M X
+// (Ifpack2_Relaxation_def.hpp:1401-1425), so the result equals Jacobi pass + SpMM bit for bit.
+// Under a halo the exchange carries X itself; ghost columns take the owner's omega d^-1,
+// imported once by prec_import_ghost_scale.
 bool crs_apply_jacobi_fused(migmres_crs &A, const migmres_prec &M, const migmres_mv &X, migmres_mv &Y) {
   migmres_ctx *c = A.ctx;
   const int n_remote = (int)A.plan.remote_lids.size();
   const int n_export = (int)A.export_lids.size();
   const bool halo = c->dist && (n_remote > 0 || n_export > 0);
-  if (!A.use_tpl || A.n_tpl_rest > 0 || halo || M.sweeps != 1 || !M.d_sdinv || M.A != &A) return false;
+  if (M.sweeps != 1 || !M.d_sdinv || M.A != &A) return false;
+  if (halo && n_remote > 0 && !M.d_gsdinv) return false;
   if (X.n_local != A.n_local || Y.n_local != A.n_local || X.ncols != Y.ncols) return false;
-  const int k = X.ncols;
-  ProfScope ps(c, K_SPMM, A.spmm_fixed_bytes + 8.0 * A.n_local * (2.0 * k + 1.0));
-  launch_spmm_tpl(c->stream, A.n_local, A.d_tpl_id, A.d_tpl_rec, A.tpl_ntpl, A.tpl_maxk, A.d_tpl_val, A.tpl_nvals,
-                  X.desc(), Y.desc(), 1.0, 0.0, M.d_sdinv);
+  crs_apply_impl(A, X, Y, 1.0, 0.0, ColScale{M.d_sdinv, M.d_gsdinv});
   return true;
+}
+
+// The owners' omega d^-1 of A's ghost columns (the fused Jacobi's ghost column scale): the
+// import of one vector through A's plan (pack the export rows, one message per neighbour,
+// unpack into ghost-slot order), done once when the preconditioner is created.  Collective
+// over the ranks that share A.
+void prec_import_ghost_scale(migmres_prec &M) {
+  migmres_crs &A = *M.A;
+  migmres_ctx *c = A.ctx;
+  const int n_remote = (int)A.plan.remote_lids.size();
+  const int n_export = (int)A.export_lids.size();
+  if (!c->dist || (n_remote == 0 && n_export == 0)) return;
+  const long long ldg = (n_remote + 1) & ~1LL;
+  double *send = nullptr, *recv = nullptr;
+  MIG_HIP(hipMalloc(&send, sizeof(double) * ((size_t)n_export + 1)));
+  MIG_HIP(hipMalloc(&recv, sizeof(double) * ((size_t)n_remote + 1)));
+  MIG_HIP(hipMalloc(&M.d_gsdinv, sizeof(double) * ((size_t)ldg + 2)));
+  MIG_HIP(hipMemsetAsync(M.d_gsdinv, 0, sizeof(double) * ((size_t)ldg + 2), c->stream));
+  const MvDesc sd{M.d_sdinv, (long long)A.n_local, nullptr, 1};
+  launch_pack(c->stream, sd, A.d_export, A.d_export_grp, n_export, send, 1);
+  c->p2p_begin(c->stream);
+  for (auto &nb : A.send_nbrs) c->p2p_send(send + nb.offset, sizeof(double) * nb.count, nb.pid);
+  for (auto &nb : A.recv_nbrs) c->p2p_recv(recv + nb.offset, sizeof(double) * nb.count, nb.pid);
+  c->p2p_end();
+  launch_unpack(c->stream, recv, A.d_remote_grp, n_remote, 1, M.d_gsdinv, ldg);
+  MIG_HIP(hipStreamSynchronize(c->stream));
+  hipFree(send);
+  hipFree(recv);
 }
 
 }  // namespace migmres

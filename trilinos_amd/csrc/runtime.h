@@ -178,6 +178,7 @@ struct migmres_prec {
   migmres_crs *A = nullptr;
   double *d_dinv = nullptr;
   double *d_sdinv = nullptr;  // omega * dinv (+2 zero entries): the fused form's column scale
+  double *d_gsdinv = nullptr; // the owners' omega * dinv of A's ghost columns (halo; ldg + 2, zero padded)
   int sweeps = 1;
   double damping = 1.0;
   long long n_apply = 0;
@@ -223,5 +224,6 @@ void crs_apply(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, double alpha,
 // followed by crs_apply.  Only where every row pair is templated and no halo is needed;
 // returns false (nothing done) otherwise.
 bool crs_apply_jacobi_fused(migmres_crs &A, const migmres_prec &M, const migmres_mv &X, migmres_mv &Y);
+void prec_import_ghost_scale(migmres_prec &M);
 
 }  // namespace migmres
