@@ -191,6 +191,10 @@ int migmres_crs_apply(migmres_crs *A, const migmres_mv *X, migmres_mv *Y, double
 #define MIGMRES_SPMM_PAIR 1
 #define MIGMRES_SPMM_SELL 2
 #define MIGMRES_SPMM_TPL 3
+/* MIGMRES_SPMM_TPL3: the template form of 27-point stencils on an even-nx grid, read with one X
+ * load per x-neighbour triple and the neighbours' halves taken from adjacent lanes
+ * (MIGMRES_NO_TPL3=1 at creation keeps MIGMRES_SPMM_TPL). */
+#define MIGMRES_SPMM_TPL3 4
 int migmres_crs_spmm_kernel(const migmres_crs *A, int *kind);
 
 /* ---------------- multivectors (Belos::MultiVecTraits) ---------------- */

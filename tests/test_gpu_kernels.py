@@ -287,3 +287,35 @@ def test_epetra_gemm_known_answers(comm, n):
     assert np.array_equal(MVT.MvNorm(Ad, ta.OneNorm), norm1)
     assert np.array_equal(MVT.MvDot(Ad, Ad), dot)
     np.testing.assert_allclose(MVT.MvNorm(Ad), np.sqrt(dot), rtol=1e-15)
+
+
+@pytest.mark.parametrize("dims,k", [((12, 11, 10), 8), ((16, 9, 7), 1), ((10, 10, 10), 3), ((14, 8, 6), 5),
+                                    ((20, 6, 5), 16), ((8, 7, 9), 9), ((2, 5, 4), 2)])
+@pytest.mark.parametrize("alpha,beta", [(1.0, 0.0), (-1.0, 1.0), (0.5, -2.0)])
+def test_spmm_tpl3_lane_shared_bit_exact(comm, dims, k, alpha, beta):
+    """27-point Brick3D on even-nx grids takes the lane-shared stencil-group kernel (one X load
+    per x-neighbour triple, the neighbours' halves by DPP wave shifts; waves of 62 outputs, so
+    several waves and boundary pairs sit in every case): bit for bit against the oracle for
+    every column count (chunks of 8, odd remainders), and Y = alpha A X + beta Y."""
+    import trilinos_amd as ta
+    from oracle import epetra as oe
+    nx, ny, nz = dims
+    n = nx * ny * nz
+    A = ta.CrsMatrix.galeri(comm, "Brick3D", nx, ny, nz)
+    assert A.spmm_kernel() == "tpl3"
+    Aor = oe.DistCrs(lambda f, m: oe.brick3d_rows(nx, ny, nz, f, m), n, 1)
+    X, _ = oe.epetra_random_mv(17, n, k)
+    Y0, _ = oe.epetra_random_mv(19, n, k)
+    Xd = _upload(ta, comm, X)
+    Yd = _upload(ta, comm, Y0)
+    A.apply(Xd, Yd, alpha, beta)
+    want = alpha * Aor.apply(X) if beta == 0.0 else alpha * Aor.apply(X) + beta * Y0
+    assert np.array_equal(Yd.download(), want)
+
+
+def test_spmm_tpl3_odd_nx_falls_back(comm):
+    """An odd nx puts row pairs across grid lines: no x-neighbour triples, so the operator
+    keeps the plain template kernel (still bit-exact, test_spmm_kernel_choice_bit_exact)."""
+    import trilinos_amd as ta
+    assert ta.CrsMatrix.galeri(comm, "Brick3D", 13, 12, 11).spmm_kernel() == "tpl"
+    assert ta.CrsMatrix.galeri(comm, "Laplace3D", 12, 12, 12).spmm_kernel() == "tpl"

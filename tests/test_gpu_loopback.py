@@ -69,6 +69,7 @@ def _gen(kind, dims):
 @pytest.mark.parametrize("kind,dims,k,P", [("Laplace3D", (16, 16, 16), 8, 2), ("Laplace2D", (37, 23, 1), 3, 3),
                                            ("Laplace3D", (9, 7, 5), 5, 4), ("random", (601, 4, 1), 8, 2),
                                            ("random", (500, 11, 1), 2, 3), ("Brick3D", (9, 8, 7), 8, 3),
+                                           ("Brick3D", (10, 8, 9), 8, 3), ("Brick3D", (12, 6, 8), 5, 2),
                                            ("random", (700, 0, 1), 4, 2)])
 def test_distributed_spmm_bit_exact(kind, dims, k, P):
     import trilinos_amd as ta

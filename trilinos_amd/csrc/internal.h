@@ -84,8 +84,9 @@ void launch_spmm_pair(hipStream_t s, int n_local, int max_keys, int rmax, const 
 // General rows: thread per row over the SELL-64 copy (make_sell64); sel lists rows.
 // xr (optional, n_local x 8 doubles): scratch for a row-interleaved copy of X's owned rows,
 // so each entry's k operands are one contiguous segment instead of k column gathers;
-// xr_ready: an earlier launch of this apply already filled it (k <= 8).
-void launch_spmm_sell(hipStream_t s, int n_local, const long long *off, const int *len, const int *scol,
+// xr_ready: an earlier launch of this apply already filled it (k <= 8).  Returns whether xr
+// holds X's columns after this call (pass it as xr_ready to the next launch of the apply).
+bool launch_spmm_sell(hipStream_t s, int n_local, const long long *off, const int *len, const int *scol,
                       const double *sval, MvDesc X, const double *ghost, long long ldg, MvDesc Y, double alpha,
                       double beta, const int *sel = nullptr, int nsel = 0, double *xr = nullptr,
                       bool xr_ready = false, ColScale cs = {});
@@ -99,6 +100,12 @@ void launch_spmm(hipStream_t s, int row_begin, int row_end, const int *rowptr, c
 void launch_spmm_tpl(hipStream_t s, int n_local, const unsigned char *tid, const int2 *rec, int ntpl, int maxk,
                      const double *vals, int nvals, MvDesc X, MvDesc Y, double alpha, double beta,
                      const double *colscale = nullptr);
+// The lane-shared form for stencil-group templates (make_stencil_groups; G = 3 or 9 groups,
+// centers[G] pair offsets, grp ntpl * G packed slot words): same pairs, same bits.  Returns
+// false (nothing launched) for a G it is not instantiated for.
+bool launch_spmm_tpl3(hipStream_t s, int n_local, const unsigned char *tid, const unsigned long long *grp, int ntpl,
+                      int G, const int *centers, const double *vals, int nvals, MvDesc X, MvDesc Y, double alpha,
+                      double beta, const double *colscale = nullptr);
 // out[r] = omega * a[r] (r < n)
 void launch_scaled_copy(hipStream_t s, const double *a, double omega, double *out, int n);
 

@@ -253,11 +253,11 @@ __global__ __launch_bounds__(256) void k_interleave(MvDesc X, int c0, int kc, in
   for (int h = 0; h < KC / 2; ++h) out[h] = d2{v[2 * h], v[2 * h + 1]};
 }
 
-void launch_spmm_sell(hipStream_t s, int n_local, const long long *off, const int *len, const int *scol,
+bool launch_spmm_sell(hipStream_t s, int n_local, const long long *off, const int *len, const int *scol,
                       const double *sval, MvDesc X, const double *ghost, long long ldg, MvDesc Y, double alpha,
                       double beta, const int *sel, int nsel, double *xr, bool xr_ready, ColScale cs) {
   const int n = sel ? nsel : n_local;
-  if (n <= 0) return;
+  if (n <= 0) return xr_ready;  // nothing launched: xr is as it was
   const int k = Y.ncols;
   const dim3 grid(cdiv(n, 256));
   for (int c0 = 0; c0 < k; c0 += 8) {
@@ -280,6 +280,7 @@ void launch_spmm_sell(hipStream_t s, int n_local, const long long *off, const in
       }
 #undef SELL_XR
       LAUNCH_CHECK();
+      xr_ready = k <= 8;  // xr holds this (only) chunk now
       continue;
     }
     if (kc == 1)
@@ -292,6 +293,7 @@ void launch_spmm_sell(hipStream_t s, int n_local, const long long *off, const in
       k_spmm_sell<8><<<grid, 256, 0, s>>>(n_local, off, len, scol, sval, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel, nullptr, cs.own, cs.ghost);
     LAUNCH_CHECK();
   }
+  return xr_ready;
 }
 
 // -------------------------------------------------------------------------------------
@@ -630,6 +632,141 @@ __global__ __launch_bounds__(256) void k_spmm_tplr(int npairs, int n_local, cons
   }
 }
 
+// -------------------------------------------------------------------------------------
+// SpMM x k over stencil-group templates (plan: make_stencil_groups, plan.cpp) -- the 27-point
+// operator.  A pair's keys form G groups of three consecutive pairs (c_g - 1, c_g, c_g + 1),
+// and the pair's lane loads only the centre pair p + c_g of each group: its left neighbour
+// lane's centre is p - 1 + c_g (= this pair's key c_g - 1) and its right neighbour's is
+// p + 1 + c_g (= key c_g + 1), so the two halves a row needs from those keys -- row 0 the high
+// half of c_g - 1, row 1 the low half of c_g + 1 -- come from the adjacent lanes by DPP wave
+// shifts (v_mov_b32_dpp wave_shr:1 / wave_shl:1) instead of loads: 9 X loads per column and
+// pair instead of 27 (the template kernel was bound by the texture addresser: TA 82 % busy,
+// 243 vector-memory instructions per 64 pairs, profiles/r3b_brick_spmm_pmc.json).  A wave
+// covers 64 consecutive pairs and writes the 62 inner ones (lanes 0 and 63 only load, for
+// their neighbours), so the shifts never cross a wave.  Per row the products are added group
+// by group, each group's three in ascending column order -- the stored order -- with the same
+// products v * x and no FMA as k_spmm: bit-identical.  With cs the centre operands are scaled
+// by (omega d^-1) before they are shared, exactly as k_jacobi forms them.
+// -------------------------------------------------------------------------------------
+struct StencilCenters {
+  int c[9];
+};
+
+__device__ __forceinline__ double dpp_from_prev_lane(double v) {  // lane i <- lane i - 1
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x138, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x138, 0xF, 0xF, true);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double dpp_from_next_lane(double v) {  // lane i <- lane i + 1
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x130, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x130, 0xF, 0xF, true);
+  return __hiloint2double(hi, lo);
+}
+
+template <int KC, int G>
+__global__ __launch_bounds__(256) void k_spmm_tpl3(int npairs, int n_local, const unsigned char *__restrict__ tid,
+                                                   const unsigned long long *__restrict__ grp, int ngrp,
+                                                   StencilCenters ctr, const double *__restrict__ vals, int nvals,
+                                                   MvDesc X, MvDesc Y, int c0, int kc, double alpha, double beta,
+                                                   const double *__restrict__ cs) {
+#pragma clang fp contract(off)
+  extern __shared__ double tpl_lds[];
+  double *s_val = tpl_lds;
+  __shared__ int s_ctr[G + 1];
+  unsigned long long *s_grp = (unsigned long long *)(tpl_lds + 256);
+  s_val[threadIdx.x] = (int)threadIdx.x < nvals ? vals[threadIdx.x] : 0.0;
+  for (int i = threadIdx.x; i < ngrp; i += 256) s_grp[i] = grp[i];
+  if (threadIdx.x <= G) s_ctr[threadIdx.x] = threadIdx.x < G ? ctr.c[threadIdx.x] : 0;
+  __syncthreads();
+  const double *xc[KC];
+  double *yc[KC];
+#pragma unroll
+  for (int c = 0; c < KC; ++c) {
+    xc[c] = colp(X, c0 + (c < kc ? c : 0));
+    yc[c] = colp(Y, c0 + (c < kc ? c : 0));
+  }
+  const int lane = threadIdx.x & 63;
+  const int nwaves = gridDim.x * 4;
+  // wave-uniform loop: every lane takes part in the shifts
+  for (int w = blockIdx.x * 4 + (int)(threadIdx.x >> 6); (long long)w * 62 < npairs; w += nwaves) {
+    const int p = w * 62 + lane - 1;
+    const bool mine = lane >= 1 && lane <= 62 && p < npairs;
+    const int t = mine ? (int)tid[p] : 0xFF;
+    const int tt = t == 0xFF ? 0 : t;  // a load-only or untemplated lane follows template 0 (unused)
+    const int pc = p < 0 ? 0 : (p >= npairs ? npairs - 1 : p);
+    double sa[KC], sb[KC];
+#pragma unroll
+    for (int c = 0; c < KC; ++c) sa[c] = sb[c] = 0.0;
+    d2 xn[KC], scn = d2{1.0, 1.0};
+    {
+      int q = pc + s_ctr[0];
+      q = q < 0 ? 0 : (q >= npairs ? npairs - 1 : q);
+#pragma unroll
+      for (int c = 0; c < KC; ++c) xn[c] = *(const d2 *)(xc[c] + 2LL * q);
+      if (cs) scn = *(const d2 *)(cs + 2LL * q);
+    }
+    // not unrolled: unrolled, the scheduler hoists all G groups' loads (512 VGPRs at KC = 8)
+#pragma unroll 1
+    for (int g = 0; g < G; ++g) {
+      d2 x[KC];
+#pragma unroll
+      for (int c = 0; c < KC; ++c) x[c] = xn[c];
+      const d2 sc = scn;
+      if (g + 1 < G) {  // the next group's loads before this group's products
+        int q = pc + s_ctr[g + 1];
+        q = q < 0 ? 0 : (q >= npairs ? npairs - 1 : q);
+#pragma unroll
+        for (int c = 0; c < KC; ++c) xn[c] = *(const d2 *)(xc[c] + 2LL * q);
+        if (cs) scn = *(const d2 *)(cs + 2LL * q);
+      }
+      if (cs) {
+#pragma unroll
+        for (int c = 0; c < KC; ++c) x[c] = sc * x[c];
+      }
+      const unsigned long long sl = s_grp[tt * G + g];
+      const unsigned s0 = sl & 0xFF, s1 = (sl >> 8) & 0xFF, s2 = (sl >> 16) & 0xFF;
+      const unsigned s3 = (sl >> 24) & 0xFF, s4 = (sl >> 32) & 0xFF, s5 = (sl >> 40) & 0xFF;
+      const double v0 = s_val[s0], v1 = s_val[s1], v2 = s_val[s2];
+      const double v3 = s_val[s3], v4 = s_val[s4], v5 = s_val[s5];
+#pragma unroll
+      for (int c = 0; c < KC; ++c) {
+        const double left = dpp_from_prev_lane(x[c].y);   // key c_g - 1, high half (row 0's x - 1)
+        const double right = dpp_from_next_lane(x[c].x);  // key c_g + 1, low half (row 1's x + 1)
+        const double pa0 = v0 * left, pa1 = v1 * x[c].x, pa2 = v2 * x[c].y;
+        const double pb0 = v3 * x[c].x, pb1 = v4 * x[c].y, pb2 = v5 * right;
+        sa[c] = sa[c] + (s0 != 0xFF ? pa0 : 0.0);
+        sa[c] = sa[c] + (s1 != 0xFF ? pa1 : 0.0);
+        sa[c] = sa[c] + (s2 != 0xFF ? pa2 : 0.0);
+        sb[c] = sb[c] + (s3 != 0xFF ? pb0 : 0.0);
+        sb[c] = sb[c] + (s4 != 0xFF ? pb1 : 0.0);
+        sb[c] = sb[c] + (s5 != 0xFF ? pb2 : 0.0);
+      }
+    }
+    if (t == 0xFF) continue;
+    const int ra = 2 * p;
+    const bool hasb = ra + 1 < n_local;
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+      if (c >= kc) break;
+      double *yp = yc[c] + ra;
+      double a = sa[c], b = sb[c];
+      if (beta == 0.0) {
+        if (alpha != 1.0) {
+          a = alpha * a;
+          b = alpha * b;
+        }
+      } else {
+        a = alpha * a + beta * yp[0];
+        if (hasb) b = alpha * b + beta * yp[1];
+      }
+      if (hasb)
+        *(d2 *)yp = d2{a, b};
+      else
+        yp[0] = a;
+    }
+  }
+}
+
 static int tpl_resident_blocks(const void *kern, size_t lds) {
   int dev = 0, ncu = 0, per_cu = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
@@ -685,6 +822,51 @@ static void tpl_cols(hipStream_t s, size_t lds, int npairs, int n_local, const u
   tpl_launch([&](int grid) { k_spmm_tpl<KC><<<grid, 256, lds, s>>>(npairs, n_local, tid, rec, maxk, nrec, vals, nvals,
                                                                   X, Y, c0, kc, alpha, beta, cs); },
              s, lds, npairs, (const void *)k_spmm_tpl<KC>);
+}
+
+template <int KC, int G>
+static void tpl3_cols(hipStream_t s, size_t lds, int npairs, int n_local, const unsigned char *tid,
+                      const unsigned long long *grp, int ngrp, StencilCenters ctr, const double *vals, int nvals,
+                      MvDesc X, MvDesc Y, int c0, int kc, double alpha, double beta, const double *cs) {
+  const int units = cdiv(npairs, 62);  // wave iterations (62 pairs each)
+  tpl_launch([&](int grid) {
+               k_spmm_tpl3<KC, G><<<grid, 256, lds, s>>>(npairs, n_local, tid, grp, ngrp, ctr, vals, nvals, X, Y,
+                                                          c0, kc, alpha, beta, cs);
+             },
+             s, lds, units * 64, (const void *)k_spmm_tpl3<KC, G>);
+}
+
+bool launch_spmm_tpl3(hipStream_t s, int n_local, const unsigned char *tid, const unsigned long long *grp, int ntpl,
+                      int G, const int *centers, const double *vals, int nvals, MvDesc X, MvDesc Y, double alpha,
+                      double beta, const double *colscale) {
+  const int npairs = (n_local + 1) / 2;
+  if (npairs <= 0) return true;
+  if (G != 9 && G != 3) return false;
+  StencilCenters ctr{};
+  for (int g = 0; g < G; ++g) ctr.c[g] = centers[g];
+  const int ngrp = ntpl * G;
+  const size_t lds = sizeof(double) * 256 + sizeof(unsigned long long) * (size_t)ngrp;
+  const int k = Y.ncols;
+  for (int c0 = 0; c0 < k; c0 += 8) {
+    const int kc = (k - c0) < 8 ? (k - c0) : 8;
+#define TPL3(KC)                                                                                                   \
+  if (G == 9)                                                                                                      \
+    tpl3_cols<KC, 9>(s, lds, npairs, n_local, tid, grp, ngrp, ctr, vals, nvals, X, Y, c0, kc, alpha, beta, colscale); \
+  else                                                                                                             \
+    tpl3_cols<KC, 3>(s, lds, npairs, n_local, tid, grp, ngrp, ctr, vals, nvals, X, Y, c0, kc, alpha, beta, colscale);
+    if (kc == 1) {
+      TPL3(1)
+    } else if (kc <= 2) {
+      TPL3(2)
+    } else if (kc <= 4) {
+      TPL3(4)
+    } else {
+      TPL3(8)
+    }
+#undef TPL3
+    LAUNCH_CHECK();
+  }
+  return true;
 }
 
 void launch_spmm_tpl(hipStream_t s, int n_local, const unsigned char *tid, const int2 *rec, int ntpl, int maxk,

@@ -520,4 +520,51 @@ void make_sell64(int n_local, const long long *rowptr, const int *lcols, const d
   }
 }
 
+bool make_stencil_groups(const PairTemplates &pt, StencilGroups &out) {
+  out = StencilGroups();
+  std::vector<int> offs;
+  for (int t = 0; t < pt.ntpl; ++t)
+    for (int u = 0; u < pt.maxk; ++u)
+      if ((unsigned)pt.rec[2 * ((size_t)t * pt.maxk + u) + 1] != 0xFFFFFFFFu)
+        offs.push_back(pt.rec[2 * ((size_t)t * pt.maxk + u)]);
+  std::sort(offs.begin(), offs.end());
+  offs.erase(std::unique(offs.begin(), offs.end()), offs.end());
+  // groups from the smallest unclaimed offset: (o, o + 1, o + 2) around centre o + 1
+  for (size_t i = 0; i < offs.size();) {
+    const int c = offs[i] + 1;
+    if (!out.center.empty() && c - out.center.back() < 3) return false;
+    out.center.push_back(c);
+    while (i < offs.size() && offs[i] <= c + 1) ++i;
+  }
+  out.G = (int)out.center.size();
+  if (out.G < 1 || out.G > 9) return false;
+  out.slots.assign((size_t)pt.ntpl * out.G, ~0ULL);
+  for (int t = 0; t < pt.ntpl; ++t)
+    for (int u = 0; u < pt.maxk; ++u) {
+      const int off = pt.rec[2 * ((size_t)t * pt.maxk + u)];
+      const unsigned sl = (unsigned)pt.rec[2 * ((size_t)t * pt.maxk + u) + 1];
+      if (sl == 0xFFFFFFFFu) continue;  // padding record
+      int g = 0;
+      while (g < out.G && !(off >= out.center[g] - 1 && off <= out.center[g] + 1)) ++g;
+      if (g == out.G) return false;
+      const int d = off - out.center[g];
+      const unsigned r0lo = sl & 0xFF, r0hi = (sl >> 8) & 0xFF, r1lo = (sl >> 16) & 0xFF, r1hi = sl >> 24;
+      unsigned long long &w = out.slots[(size_t)t * out.G + g];
+      auto put = [&](int byte, unsigned v) { w = (w & ~(0xFFULL << (8 * byte))) | ((unsigned long long)v << (8 * byte)); };
+      if (d == -1) {
+        if (r0lo != kTplUnused || r1lo != kTplUnused || r1hi != kTplUnused) return false;
+        put(0, r0hi);
+      } else if (d == 0) {
+        put(1, r0lo);
+        put(2, r0hi);
+        put(3, r1lo);
+        put(4, r1hi);
+      } else {
+        if (r0lo != kTplUnused || r0hi != kTplUnused || r1hi != kTplUnused) return false;
+        put(5, r1lo);
+      }
+    }
+  return true;
+}
+
 }  // namespace migmres

@@ -99,6 +99,23 @@ struct PairTemplates {
 bool make_pair_templates(int n_local, const long long *rowptr, const int *xcols, const double *lvals,
                          PairTemplates &out);
 
+// Lane-shared form of the templates for k_spmm_tpl3 (kernels.hip): every key offset of every
+// template lies in one of G groups of three consecutive pair offsets (c_g - 1, c_g, c_g + 1)
+// -- the x-neighbours along one (dy, dz) line of a 3-D stencil on an even-nx grid -- and each
+// row reads only the halves a 3-point line stencil reads: row 0 (even x) the high half of
+// c_g - 1 and both halves of c_g; row 1 both halves of c_g and the low half of c_g + 1.  A
+// lane then loads only the centre pair of each group and takes the neighbours' halves from the
+// adjacent lanes.  slots[(t * G + g)] packs the group's six value-dictionary slots (bytes 0-5:
+// row 0 from c-1 high, c low, c high; row 1 from c low, c high, c+1 low; kTplUnused = none).
+// Groups must be at least 3 apart so each row's sums keep their stored (ascending) order.
+// Returns false when the templates do not have this shape.
+struct StencilGroups {
+  int G = 0;
+  std::vector<int> center;
+  std::vector<unsigned long long> slots;
+};
+bool make_stencil_groups(const PairTemplates &pt, StencilGroups &out);
+
 void galeri_rows(const std::string &kind, int nx, int ny, int nz, long long first, int n_local,
                  std::vector<long long> &rowptr, std::vector<long long> &gcols,
                  std::vector<double> &vals);

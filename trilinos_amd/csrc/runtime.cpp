@@ -707,7 +707,7 @@ void mv_assign(const migmres_mv &A, migmres_mv &Y) {
 // ------------------------------------------------------------------------------------
 migmres_crs::~migmres_crs() {
   for (void *p : {(void *)d_soff, (void *)d_slen, (void *)d_scol, (void *)d_sval, (void *)d_xr, (void *)d_tpl_id,
-                  (void *)d_tpl_rec, (void *)d_tpl_val, (void *)d_tpl_rest})
+                  (void *)d_tpl_rec, (void *)d_tpl_val, (void *)d_tpl_rest, (void *)d_tpl3_grp})
     if (p) hipFree(p);
   for (void *p : {(void *)d_export_grp, (void *)d_remote_grp, (void *)d_recv})
     if (p) hipFree(p);
@@ -930,6 +930,18 @@ static void crs_finish(migmres_crs *A, const long long *rowptr, std::vector<int>
         A->tpl_maxk = pt.maxk;
         A->tpl_nvals = (int)pt.vals.size();
         A->use_tpl = true;
+        // long templates (27-point stencils): the lane-shared form when the keys come in
+        // x-neighbour triples (k_spmm_tpl3); MIGMRES_NO_TPL3=1 keeps k_spmm_tpl
+        const char *n3 = std::getenv("MIGMRES_NO_TPL3");
+        StencilGroups sg;
+        if (!(n3 && n3[0] == '1') && pt.maxk > 12 && make_stencil_groups(pt, sg) && (sg.G == 9 || sg.G == 3)) {
+          MIG_HIP(hipMalloc(&A->d_tpl3_grp, sizeof(unsigned long long) * sg.slots.size()));
+          MIG_HIP(hipMemcpy(A->d_tpl3_grp, sg.slots.data(), sizeof(unsigned long long) * sg.slots.size(),
+                            hipMemcpyHostToDevice));
+          A->tpl3_center = sg.center;
+          A->tpl3_G = sg.G;
+          A->use_tpl3 = true;
+        }
         A->spmm_fixed_bytes = (double)pt.npairs + 8.0 * pt.rec.size() / 2 + 8.0 * pt.vals.size() + rest_bytes;
       }
     }
@@ -1006,9 +1018,8 @@ static void crs_apply_impl(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, d
       launch_spmm_pair(c->stream, A.n_local, A.pair_max_keys, A.pair_rmax, A.d_psv, A.d_psk, A.d_psm, X.desc(),
                        A.d_ghost, A.ldg, Y.desc(), alpha, beta, sel, nsel, cs);
     } else if (A.use_sell) {
-      launch_spmm_sell(c->stream, A.n_local, A.d_soff, A.d_slen, A.d_scol, A.d_sval, X.desc(), A.d_ghost, A.ldg,
-                       Y.desc(), alpha, beta, sel, nsel, xr, xr_ready, cs);
-      xr_ready = xr != nullptr;
+      xr_ready = launch_spmm_sell(c->stream, A.n_local, A.d_soff, A.d_slen, A.d_scol, A.d_sval, X.desc(),
+                                  A.d_ghost, A.ldg, Y.desc(), alpha, beta, sel, nsel, xr, xr_ready, cs);
     } else {
       launch_spmm(c->stream, 0, A.n_local, A.d_rowptr, A.d_cols, A.d_vals, X.desc(), A.n_local, A.d_ghost, A.ldg,
                   Y.desc(), alpha, beta, sel, nsel, cs);
@@ -1054,8 +1065,11 @@ static void crs_apply_impl(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, d
   if (A.use_tpl) {
     // templated pairs read no ghost column: they run while the halo is in flight, then the
     // pairs that do read one go to the fallback kernel
-    launch_spmm_tpl(c->stream, A.n_local, A.d_tpl_id, A.d_tpl_rec, A.tpl_ntpl, A.tpl_maxk, A.d_tpl_val,
-                    A.tpl_nvals, X.desc(), Y.desc(), alpha, beta, cs.own);
+    if (!A.use_tpl3 || !launch_spmm_tpl3(c->stream, A.n_local, A.d_tpl_id, A.d_tpl3_grp, A.tpl_ntpl, A.tpl3_G,
+                                         A.tpl3_center.data(), A.d_tpl_val, A.tpl_nvals, X.desc(), Y.desc(),
+                                         alpha, beta, cs.own))
+      launch_spmm_tpl(c->stream, A.n_local, A.d_tpl_id, A.d_tpl_rec, A.tpl_ntpl, A.tpl_maxk, A.d_tpl_val,
+                      A.tpl_nvals, X.desc(), Y.desc(), alpha, beta, cs.own);
     if (halo) MIG_HIP(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
     if (A.n_tpl_rest > 0) spmm(A.d_tpl_rest, A.n_tpl_rest);
   } else if (halo && A.d_sel_int) {
@@ -1126,7 +1140,8 @@ void prec_import_ghost_scale(migmres_prec &M) {
 extern "C" int migmres_crs_spmm_kernel(const migmres_crs *A, int *kind) {
   return guard([&] {
     MIG_CHECK(A && kind, "bad arguments");
-    *kind = A->use_tpl ? MIGMRES_SPMM_TPL
+    *kind = A->use_tpl3 ? MIGMRES_SPMM_TPL3
+            : A->use_tpl ? MIGMRES_SPMM_TPL
             : A->use_pairs ? MIGMRES_SPMM_PAIR
             : A->use_sell  ? MIGMRES_SPMM_SELL
                            : MIGMRES_SPMM_CSR;

@@ -159,6 +159,12 @@ struct migmres_crs {
   int tpl_ntpl = 0, tpl_maxk = 0, tpl_nvals = 0;
   bool use_tpl = false;
   int *d_tpl_rest = nullptr;
+  // stencil-group form of the templates (k_spmm_tpl3: one X load per key triple, the
+  // neighbours' halves by DPP lane shifts) when the keys come in x-neighbour triples
+  unsigned long long *d_tpl3_grp = nullptr;
+  std::vector<int> tpl3_center;
+  int tpl3_G = 0;
+  bool use_tpl3 = false;
   int n_tpl_rest = 0;
   double spmm_fixed_bytes = 0.0;  // matrix-format bytes one apply reads (bench accounting)
   // interior / boundary split (units = pairs with the row-pair kernel, else rows): interior

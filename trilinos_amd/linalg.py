@@ -176,10 +176,11 @@ class CrsMatrix:
         return cls(comm, ng.value, _handle=h)
 
     def spmm_kernel(self):
-        """The SpMM kernel apply() runs: "csr", "pair", "sell" or "tpl" (migmres_crs_spmm_kernel)."""
+        """The SpMM kernel apply() runs: "csr", "pair", "sell", "tpl" or "tpl3"
+        (migmres_crs_spmm_kernel)."""
         v = C.c_int()
         call("migmres_crs_spmm_kernel", self.h, C.byref(v))
-        return ("csr", "pair", "sell", "tpl")[v.value]
+        return ("csr", "pair", "sell", "tpl", "tpl3")[v.value]
 
     def colmap(self):
         out = np.empty(self.n_cols, dtype=np.int64)
