@@ -290,7 +290,7 @@ def test_epetra_gemm_known_answers(comm, n):
 
 
 @pytest.mark.parametrize("dims,k", [((12, 11, 10), 8), ((16, 9, 7), 1), ((10, 10, 10), 3), ((14, 8, 6), 5),
-                                    ((20, 6, 5), 16), ((8, 7, 9), 9), ((2, 5, 4), 2)])
+                                    ((20, 6, 5), 16), ((8, 7, 9), 9), ((6, 5, 4), 2)])
 @pytest.mark.parametrize("alpha,beta", [(1.0, 0.0), (-1.0, 1.0), (0.5, -2.0)])
 def test_spmm_tpl3_lane_shared_bit_exact(comm, dims, k, alpha, beta):
     """27-point Brick3D on even-nx grids takes the lane-shared stencil-group kernel (one X load

@@ -105,7 +105,7 @@ void launch_spmm_tpl(hipStream_t s, int n_local, const unsigned char *tid, const
 // false (nothing launched) for a G it is not instantiated for.
 bool launch_spmm_tpl3(hipStream_t s, int n_local, const unsigned char *tid, const unsigned long long *grp, int ntpl,
                       int G, const int *centers, const double *vals, int nvals, MvDesc X, MvDesc Y, double alpha,
-                      double beta, const double *colscale = nullptr);
+                      double beta, const double *colscale = nullptr, int xcd_slabs = 0, int kcmax = 8);
 // out[r] = omega * a[r] (r < n)
 void launch_scaled_copy(hipStream_t s, const double *a, double omega, double *out, int n);
 

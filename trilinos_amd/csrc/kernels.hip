@@ -668,7 +668,7 @@ __global__ __launch_bounds__(256) void k_spmm_tpl3(int npairs, int n_local, cons
                                                    const unsigned long long *__restrict__ grp, int ngrp,
                                                    StencilCenters ctr, const double *__restrict__ vals, int nvals,
                                                    MvDesc X, MvDesc Y, int c0, int kc, double alpha, double beta,
-                                                   const double *__restrict__ cs) {
+                                                   const double *__restrict__ cs, int xcd_slabs) {
 #pragma clang fp contract(off)
   extern __shared__ double tpl_lds[];
   double *s_val = tpl_lds;
@@ -686,9 +686,23 @@ __global__ __launch_bounds__(256) void k_spmm_tpl3(int npairs, int n_local, cons
     yc[c] = colp(Y, c0 + (c < kc ? c : 0));
   }
   const int lane = threadIdx.x & 63;
-  const int nwaves = gridDim.x * 4;
+  // wave items of 62 pairs: grid-stride over all of them, or (xcd_slabs; workgroups are
+  // dealt to the 8 XCDs round-robin) each XCD walks a contiguous eighth, so the neighbouring
+  // lines and planes a stencil row reads were mostly fetched into the same XCD's L2
+  const int items = (npairs + 61) / 62;
+  int w0, w1, ws;
+  if (xcd_slabs) {
+    const int xcd = blockIdx.x & 7, nb = gridDim.x >> 3;
+    w0 = (int)((long long)items * xcd / 8) + (int)(blockIdx.x >> 3) * 4 + (int)(threadIdx.x >> 6);
+    w1 = (int)((long long)items * (xcd + 1) / 8);
+    ws = nb * 4;
+  } else {
+    w0 = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+    w1 = items;
+    ws = gridDim.x * 4;
+  }
   // wave-uniform loop: every lane takes part in the shifts
-  for (int w = blockIdx.x * 4 + (int)(threadIdx.x >> 6); (long long)w * 62 < npairs; w += nwaves) {
+  for (int w = w0; w < w1; w += ws) {
     const int p = w * 62 + lane - 1;
     const bool mine = lane >= 1 && lane <= 62 && p < npairs;
     const int t = mine ? (int)tid[p] : 0xFF;
@@ -827,18 +841,22 @@ static void tpl_cols(hipStream_t s, size_t lds, int npairs, int n_local, const u
 template <int KC, int G>
 static void tpl3_cols(hipStream_t s, size_t lds, int npairs, int n_local, const unsigned char *tid,
                       const unsigned long long *grp, int ngrp, StencilCenters ctr, const double *vals, int nvals,
-                      MvDesc X, MvDesc Y, int c0, int kc, double alpha, double beta, const double *cs) {
+                      MvDesc X, MvDesc Y, int c0, int kc, double alpha, double beta, const double *cs,
+                      int xcd_slabs) {
   const int units = cdiv(npairs, 62);  // wave iterations (62 pairs each)
   tpl_launch([&](int grid) {
+               // the slab walk needs whole rounds of 8 workgroups (one per XCD)
+               const bool slabs = xcd_slabs && grid >= 64;
+               if (slabs) grid &= ~7;
                k_spmm_tpl3<KC, G><<<grid, 256, lds, s>>>(npairs, n_local, tid, grp, ngrp, ctr, vals, nvals, X, Y,
-                                                          c0, kc, alpha, beta, cs);
+                                                          c0, kc, alpha, beta, cs, slabs ? 1 : 0);
              },
              s, lds, units * 64, (const void *)k_spmm_tpl3<KC, G>);
 }
 
 bool launch_spmm_tpl3(hipStream_t s, int n_local, const unsigned char *tid, const unsigned long long *grp, int ntpl,
                       int G, const int *centers, const double *vals, int nvals, MvDesc X, MvDesc Y, double alpha,
-                      double beta, const double *colscale) {
+                      double beta, const double *colscale, int xcd_slabs, int kcmax) {
   const int npairs = (n_local + 1) / 2;
   if (npairs <= 0) return true;
   if (G != 9 && G != 3) return false;
@@ -847,13 +865,16 @@ bool launch_spmm_tpl3(hipStream_t s, int n_local, const unsigned char *tid, cons
   const int ngrp = ntpl * G;
   const size_t lds = sizeof(double) * 256 + sizeof(unsigned long long) * (size_t)ngrp;
   const int k = Y.ncols;
-  for (int c0 = 0; c0 < k; c0 += 8) {
-    const int kc = (k - c0) < 8 ? (k - c0) : 8;
+  const int kstep = kcmax == 4 ? 4 : 8;
+  for (int c0 = 0; c0 < k; c0 += kstep) {
+    const int kc = (k - c0) < kstep ? (k - c0) : kstep;
 #define TPL3(KC)                                                                                                   \
   if (G == 9)                                                                                                      \
-    tpl3_cols<KC, 9>(s, lds, npairs, n_local, tid, grp, ngrp, ctr, vals, nvals, X, Y, c0, kc, alpha, beta, colscale); \
+    tpl3_cols<KC, 9>(s, lds, npairs, n_local, tid, grp, ngrp, ctr, vals, nvals, X, Y, c0, kc, alpha, beta, colscale, \
+                     xcd_slabs);                                                                                   \
   else                                                                                                             \
-    tpl3_cols<KC, 3>(s, lds, npairs, n_local, tid, grp, ngrp, ctr, vals, nvals, X, Y, c0, kc, alpha, beta, colscale);
+    tpl3_cols<KC, 3>(s, lds, npairs, n_local, tid, grp, ngrp, ctr, vals, nvals, X, Y, c0, kc, alpha, beta, colscale, \
+                     xcd_slabs);
     if (kc == 1) {
       TPL3(1)
     } else if (kc <= 2) {

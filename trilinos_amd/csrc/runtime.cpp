@@ -941,6 +941,10 @@ static void crs_finish(migmres_crs *A, const long long *rowptr, std::vector<int>
           A->tpl3_center = sg.center;
           A->tpl3_G = sg.G;
           A->use_tpl3 = true;
+          const char *sl = std::getenv("MIGMRES_TPL3_SLABS");
+          A->tpl3_slabs = sl ? std::atoi(sl) : 0;
+          const char *kc = std::getenv("MIGMRES_TPL3_KC");
+          A->tpl3_kc = kc ? std::atoi(kc) : 8;
         }
         A->spmm_fixed_bytes = (double)pt.npairs + 8.0 * pt.rec.size() / 2 + 8.0 * pt.vals.size() + rest_bytes;
       }
@@ -1067,7 +1071,7 @@ static void crs_apply_impl(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, d
     // pairs that do read one go to the fallback kernel
     if (!A.use_tpl3 || !launch_spmm_tpl3(c->stream, A.n_local, A.d_tpl_id, A.d_tpl3_grp, A.tpl_ntpl, A.tpl3_G,
                                          A.tpl3_center.data(), A.d_tpl_val, A.tpl_nvals, X.desc(), Y.desc(),
-                                         alpha, beta, cs.own))
+                                         alpha, beta, cs.own, A.tpl3_slabs, A.tpl3_kc))
       launch_spmm_tpl(c->stream, A.n_local, A.d_tpl_id, A.d_tpl_rec, A.tpl_ntpl, A.tpl_maxk, A.d_tpl_val,
                       A.tpl_nvals, X.desc(), Y.desc(), alpha, beta, cs.own);
     if (halo) MIG_HIP(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
