@@ -99,7 +99,7 @@ void launch_spmm(hipStream_t s, int row_begin, int row_end, const int *rowptr, c
 // operand exactly as k_jacobi forms (omega D^-1) X (the right Jacobi preconditioner fused).
 void launch_spmm_tpl(hipStream_t s, int n_local, const unsigned char *tid, const int2 *rec, int ntpl, int maxk,
                      const double *vals, int nvals, MvDesc X, MvDesc Y, double alpha, double beta,
-                     const double *colscale = nullptr);
+                     const double *colscale = nullptr, int xcd_slabs = 0, int kcmax = 8);
 // The lane-shared form for stencil-group templates (make_stencil_groups; G = 3 or 9 groups,
 // centers[G] pair offsets, grp ntpl * G packed slot words): same pairs, same bits.  Returns
 // false (nothing launched) for a G it is not instantiated for.

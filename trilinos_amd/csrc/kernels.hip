@@ -561,7 +561,7 @@ __global__ __launch_bounds__(256) void k_spmm_tplr(int npairs, int n_local, cons
                                                    const int2 *__restrict__ rec, int nrec,
                                                    const double *__restrict__ vals, int nvals, MvDesc X, MvDesc Y,
                                                    int c0, int kc, double alpha, double beta,
-                                                   const double *__restrict__ cs) {
+                                                   const double *__restrict__ cs, int xcd_slabs) {
 #pragma clang fp contract(off)
   extern __shared__ double tpl_lds[];
   double *s_val = tpl_lds;
@@ -569,7 +569,20 @@ __global__ __launch_bounds__(256) void k_spmm_tplr(int npairs, int n_local, cons
   s_val[threadIdx.x] = (int)threadIdx.x < nvals ? vals[threadIdx.x] : 0.0;
   for (int i = threadIdx.x; i < nrec; i += 256) s_rec[i] = rec[i];
   __syncthreads();
-  for (int p = blockIdx.x * 256 + threadIdx.x; p < npairs; p += gridDim.x * 256) {
+  // grid-stride, or (xcd_slabs) each XCD a contiguous eighth of the pairs in 256-pair blocks
+  int p0, p1, ps;
+  if (xcd_slabs) {
+    const int xcd = blockIdx.x & 7, nb = gridDim.x >> 3;
+    const int blocks = (npairs + 255) / 256;
+    p0 = ((int)((long long)blocks * xcd / 8) + (int)(blockIdx.x >> 3)) * 256 + threadIdx.x;
+    p1 = min(npairs, (int)((long long)blocks * (xcd + 1) / 8) * 256);
+    ps = nb * 256;
+  } else {
+    p0 = blockIdx.x * 256 + threadIdx.x;
+    p1 = npairs;
+    ps = gridDim.x * 256;
+  }
+  for (int p = p0; p < p1; p += ps) {
     const int t = tid[p];
     if (t == 0xFF) continue;
     int key[MAXK];
@@ -809,11 +822,15 @@ static void tpl_launch(K kern, hipStream_t s, size_t lds, int npairs, const void
 template <int KC>
 static void tpl_cols(hipStream_t s, size_t lds, int npairs, int n_local, const unsigned char *tid, const int2 *rec,
                      int maxk, int nrec, const double *vals, int nvals, MvDesc X, MvDesc Y, int c0, int kc,
-                     double alpha, double beta, const double *cs) {
+                     double alpha, double beta, const double *cs, int xcd_slabs) {
 #define TPLR_CASE(K)                                                                                          \
   case K:                                                                                                     \
-    tpl_launch([&](int grid) { k_spmm_tplr<KC, K><<<grid, 256, lds, s>>>(npairs, n_local, tid, rec, nrec, vals, \
-                                                                        nvals, X, Y, c0, kc, alpha, beta, cs); }, \
+    tpl_launch([&](int grid) {                                                                                \
+                 const bool slabs = xcd_slabs && grid >= 64;                                                  \
+                 if (slabs) grid &= ~7;                                                                       \
+                 k_spmm_tplr<KC, K><<<grid, 256, lds, s>>>(npairs, n_local, tid, rec, nrec, vals, nvals, X, Y, \
+                                                           c0, kc, alpha, beta, cs, slabs ? 1 : 0);           \
+               },                                                                                             \
                s, lds, npairs, (const void *)k_spmm_tplr<KC, K>);                                             \
     return;
   switch (maxk) {
@@ -865,7 +882,7 @@ bool launch_spmm_tpl3(hipStream_t s, int n_local, const unsigned char *tid, cons
   const int ngrp = ntpl * G;
   const size_t lds = sizeof(double) * 256 + sizeof(unsigned long long) * (size_t)ngrp;
   const int k = Y.ncols;
-  const int kstep = kcmax == 4 ? 4 : 8;
+  const int kstep = kcmax == 2 ? 2 : kcmax == 4 ? 4 : 8;
   for (int c0 = 0; c0 < k; c0 += kstep) {
     const int kc = (k - c0) < kstep ? (k - c0) : kstep;
 #define TPL3(KC)                                                                                                   \
@@ -892,22 +909,23 @@ bool launch_spmm_tpl3(hipStream_t s, int n_local, const unsigned char *tid, cons
 
 void launch_spmm_tpl(hipStream_t s, int n_local, const unsigned char *tid, const int2 *rec, int ntpl, int maxk,
                      const double *vals, int nvals, MvDesc X, MvDesc Y, double alpha, double beta,
-                     const double *colscale) {
+                     const double *colscale, int xcd_slabs, int kcmax) {
   const int npairs = (n_local + 1) / 2;
   if (npairs <= 0) return;
   const int nrec = ntpl * maxk;
   const size_t lds = sizeof(double) * 256 + sizeof(int2) * (size_t)nrec;
   const int k = Y.ncols;
-  for (int c0 = 0; c0 < k; c0 += 8) {
-    const int kc = (k - c0) < 8 ? (k - c0) : 8;
+  const int kstep = kcmax == 2 ? 2 : kcmax == 4 ? 4 : 8;
+  for (int c0 = 0; c0 < k; c0 += kstep) {
+    const int kc = (k - c0) < kstep ? (k - c0) : kstep;
     if (kc == 1)
-      tpl_cols<1>(s, lds, npairs, n_local, tid, rec, maxk, nrec, vals, nvals, X, Y, c0, kc, alpha, beta, colscale);
+      tpl_cols<1>(s, lds, npairs, n_local, tid, rec, maxk, nrec, vals, nvals, X, Y, c0, kc, alpha, beta, colscale, xcd_slabs);
     else if (kc <= 2)
-      tpl_cols<2>(s, lds, npairs, n_local, tid, rec, maxk, nrec, vals, nvals, X, Y, c0, kc, alpha, beta, colscale);
+      tpl_cols<2>(s, lds, npairs, n_local, tid, rec, maxk, nrec, vals, nvals, X, Y, c0, kc, alpha, beta, colscale, xcd_slabs);
     else if (kc <= 4)
-      tpl_cols<4>(s, lds, npairs, n_local, tid, rec, maxk, nrec, vals, nvals, X, Y, c0, kc, alpha, beta, colscale);
+      tpl_cols<4>(s, lds, npairs, n_local, tid, rec, maxk, nrec, vals, nvals, X, Y, c0, kc, alpha, beta, colscale, xcd_slabs);
     else
-      tpl_cols<8>(s, lds, npairs, n_local, tid, rec, maxk, nrec, vals, nvals, X, Y, c0, kc, alpha, beta, colscale);
+      tpl_cols<8>(s, lds, npairs, n_local, tid, rec, maxk, nrec, vals, nvals, X, Y, c0, kc, alpha, beta, colscale, xcd_slabs);
     LAUNCH_CHECK();
   }
 }

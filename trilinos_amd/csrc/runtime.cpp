@@ -930,6 +930,10 @@ static void crs_finish(migmres_crs *A, const long long *rowptr, std::vector<int>
         A->tpl_maxk = pt.maxk;
         A->tpl_nvals = (int)pt.vals.size();
         A->use_tpl = true;
+        const char *tsl = std::getenv("MIGMRES_TPL_SLABS");
+        A->tpl_slabs = tsl ? std::atoi(tsl) : 0;
+        const char *tkc = std::getenv("MIGMRES_TPL_KC");
+        A->tpl_kc = tkc ? std::atoi(tkc) : 8;
         // long templates (27-point stencils): the lane-shared form when the keys come in
         // x-neighbour triples (k_spmm_tpl3); MIGMRES_NO_TPL3=1 keeps k_spmm_tpl
         const char *n3 = std::getenv("MIGMRES_NO_TPL3");
@@ -1073,7 +1077,7 @@ static void crs_apply_impl(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, d
                                          A.tpl3_center.data(), A.d_tpl_val, A.tpl_nvals, X.desc(), Y.desc(),
                                          alpha, beta, cs.own, A.tpl3_slabs, A.tpl3_kc))
       launch_spmm_tpl(c->stream, A.n_local, A.d_tpl_id, A.d_tpl_rec, A.tpl_ntpl, A.tpl_maxk, A.d_tpl_val,
-                      A.tpl_nvals, X.desc(), Y.desc(), alpha, beta, cs.own);
+                      A.tpl_nvals, X.desc(), Y.desc(), alpha, beta, cs.own, A.tpl_slabs, A.tpl_kc);
     if (halo) MIG_HIP(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
     if (A.n_tpl_rest > 0) spmm(A.d_tpl_rest, A.n_tpl_rest);
   } else if (halo && A.d_sel_int) {

@@ -166,6 +166,7 @@ struct migmres_crs {
   int tpl3_G = 0;
   bool use_tpl3 = false;
   int tpl3_slabs = 0, tpl3_kc = 8;  // walk order (XCD slabs) and columns per launch (tuning)
+  int tpl_slabs = 0, tpl_kc = 8;
   int n_tpl_rest = 0;
   double spmm_fixed_bytes = 0.0;  // matrix-format bytes one apply reads (bench accounting)
   // interior / boundary split (units = pairs with the row-pair kernel, else rows): interior
