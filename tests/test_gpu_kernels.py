@@ -319,3 +319,21 @@ def test_spmm_tpl3_odd_nx_falls_back(comm):
     import trilinos_amd as ta
     assert ta.CrsMatrix.galeri(comm, "Brick3D", 13, 12, 11).spmm_kernel() == "tpl"
     assert ta.CrsMatrix.galeri(comm, "Laplace3D", 12, 12, 12).spmm_kernel() == "tpl"
+
+
+@pytest.mark.parametrize("dims,k", [((12, 11, 10), 8), ((16, 9, 7), 3), ((8, 7, 9), 9)])
+def test_spmm_tpl3_seven_point_bit_exact(comm, dims, k, monkeypatch):
+    """The 7-point operator in stencil-group form (MIGMRES_TPL3_SHORT=1: five groups, the x
+    triple plus four single y/z keys): bit for bit against the oracle."""
+    import trilinos_amd as ta
+    from oracle import epetra as oe
+    monkeypatch.setenv("MIGMRES_TPL3_SHORT", "1")
+    nx, ny, nz = dims
+    n = nx * ny * nz
+    A = ta.CrsMatrix.galeri(comm, "Laplace3D", nx, ny, nz)
+    assert A.spmm_kernel() == "tpl3"
+    Aor = oe.DistCrs(lambda f, m: oe.laplace3d_rows(nx, ny, nz, f, m), n, 1)
+    X, _ = oe.epetra_random_mv(23, n, k)
+    Yd = ta.MultiVector(comm, n, k)
+    A.apply(_upload(ta, comm, X), Yd)
+    assert np.array_equal(Yd.download(), Aor.apply(X))

@@ -876,7 +876,7 @@ bool launch_spmm_tpl3(hipStream_t s, int n_local, const unsigned char *tid, cons
                       double beta, const double *colscale, int xcd_slabs, int kcmax) {
   const int npairs = (n_local + 1) / 2;
   if (npairs <= 0) return true;
-  if (G != 9 && G != 3) return false;
+  if (G != 9 && G != 5 && G != 3) return false;
   StencilCenters ctr{};
   for (int g = 0; g < G; ++g) ctr.c[g] = centers[g];
   const int ngrp = ntpl * G;
@@ -888,6 +888,9 @@ bool launch_spmm_tpl3(hipStream_t s, int n_local, const unsigned char *tid, cons
 #define TPL3(KC)                                                                                                   \
   if (G == 9)                                                                                                      \
     tpl3_cols<KC, 9>(s, lds, npairs, n_local, tid, grp, ngrp, ctr, vals, nvals, X, Y, c0, kc, alpha, beta, colscale, \
+                     xcd_slabs);                                                                                   \
+  else if (G == 5)                                                                                                 \
+    tpl3_cols<KC, 5>(s, lds, npairs, n_local, tid, grp, ngrp, ctr, vals, nvals, X, Y, c0, kc, alpha, beta, colscale, \
                      xcd_slabs);                                                                                   \
   else                                                                                                             \
     tpl3_cols<KC, 3>(s, lds, npairs, n_local, tid, grp, ngrp, ctr, vals, nvals, X, Y, c0, kc, alpha, beta, colscale, \

@@ -529,15 +529,19 @@ bool make_stencil_groups(const PairTemplates &pt, StencilGroups &out) {
         offs.push_back(pt.rec[2 * ((size_t)t * pt.maxk + u)]);
   std::sort(offs.begin(), offs.end());
   offs.erase(std::unique(offs.begin(), offs.end()), offs.end());
-  // groups from the smallest unclaimed offset: (o, o + 1, o + 2) around centre o + 1
+  // groups from the smallest unclaimed offset o: (o, o + 1, o + 2) around centre o + 1 when
+  // o + 1 is a key, else o alone as a centre (a y- or z-neighbour of a 7-point stencil)
   for (size_t i = 0; i < offs.size();) {
-    const int c = offs[i] + 1;
+    const bool run = i + 1 < offs.size() && offs[i + 1] == offs[i] + 1;
+    const int c = run ? offs[i] + 1 : offs[i];
     if (!out.center.empty() && c - out.center.back() < 3) return false;
     out.center.push_back(c);
     while (i < offs.size() && offs[i] <= c + 1) ++i;
   }
   out.G = (int)out.center.size();
   if (out.G < 1 || out.G > 9) return false;
+  for (size_t g = 1; g < out.center.size(); ++g)
+    if (out.center[g] - out.center[g - 1] < 3) return false;
   out.slots.assign((size_t)pt.ntpl * out.G, ~0ULL);
   for (int t = 0; t < pt.ntpl; ++t)
     for (int u = 0; u < pt.maxk; ++u) {

@@ -937,8 +937,11 @@ static void crs_finish(migmres_crs *A, const long long *rowptr, std::vector<int>
         // long templates (27-point stencils): the lane-shared form when the keys come in
         // x-neighbour triples (k_spmm_tpl3); MIGMRES_NO_TPL3=1 keeps k_spmm_tpl
         const char *n3 = std::getenv("MIGMRES_NO_TPL3");
+        const char *s3 = std::getenv("MIGMRES_TPL3_SHORT");  // 7-point templates too (tuning)
+        const bool short_ok = s3 && s3[0] == '1';
         StencilGroups sg;
-        if (!(n3 && n3[0] == '1') && pt.maxk > 12 && make_stencil_groups(pt, sg) && (sg.G == 9 || sg.G == 3)) {
+        if (!(n3 && n3[0] == '1') && (pt.maxk > 12 || short_ok) && make_stencil_groups(pt, sg) &&
+            (sg.G == 9 || sg.G == 5 || sg.G == 3)) {
           MIG_HIP(hipMalloc(&A->d_tpl3_grp, sizeof(unsigned long long) * sg.slots.size()));
           MIG_HIP(hipMemcpy(A->d_tpl3_grp, sg.slots.data(), sizeof(unsigned long long) * sg.slots.size(),
                             hipMemcpyHostToDevice));
@@ -946,9 +949,9 @@ static void crs_finish(migmres_crs *A, const long long *rowptr, std::vector<int>
           A->tpl3_G = sg.G;
           A->use_tpl3 = true;
           const char *sl = std::getenv("MIGMRES_TPL3_SLABS");
-          A->tpl3_slabs = sl ? std::atoi(sl) : 0;
+          A->tpl3_slabs = sl ? std::atoi(sl) : 1;
           const char *kc = std::getenv("MIGMRES_TPL3_KC");
-          A->tpl3_kc = kc ? std::atoi(kc) : 8;
+          A->tpl3_kc = kc ? std::atoi(kc) : 4;
         }
         A->spmm_fixed_bytes = (double)pt.npairs + 8.0 * pt.rec.size() / 2 + 8.0 * pt.vals.size() + rest_bytes;
       }
