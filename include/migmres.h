@@ -195,6 +195,10 @@ int migmres_crs_apply(migmres_crs *A, const migmres_mv *X, migmres_mv *Y, double
  * load per x-neighbour triple and the neighbours' halves taken from adjacent lanes
  * (MIGMRES_NO_TPL3=1 at creation keeps MIGMRES_SPMM_TPL). */
 #define MIGMRES_SPMM_TPL3 4
+/* MIGMRES_SPMM_BSR3: 3 x 3 block rows detected from the CRS (rows in triples sharing whole
+ * column triples, e.g. 3-dof meshes), one thread per block row; the other rows through the
+ * SELL kernel (MIGMRES_NO_BSR3=1 at creation keeps MIGMRES_SPMM_SELL). */
+#define MIGMRES_SPMM_BSR3 5
 int migmres_crs_spmm_kernel(const migmres_crs *A, int *kind);
 
 /* ---------------- multivectors (Belos::MultiVecTraits) ---------------- */

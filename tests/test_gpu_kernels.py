@@ -337,3 +337,60 @@ def test_spmm_tpl3_seven_point_bit_exact(comm, dims, k, monkeypatch):
     Yd = ta.MultiVector(comm, n, k)
     A.apply(_upload(ta, comm, X), Yd)
     assert np.array_equal(Yd.download(), Aor.apply(X))
+
+
+@pytest.mark.parametrize("dims,k", [((9, 8, 7), 4), ((11, 9, 8), 1), ((9, 7, 10), 3), ((7, 8, 6), 8), ((9, 6, 5), 9),
+                                    ((5, 4, 3), 2)])
+@pytest.mark.parametrize("alpha,beta", [(1.0, 0.0), (-1.0, 1.0)])
+def test_spmm_bsr3_bit_exact(comm, dims, k, alpha, beta):
+    """FlanProxy (3 dofs per node, configs[3]'s shape) is detected as 3 x 3 block rows
+    (migmres_crs_spmm_kernel "bsr3"): bit for bit against the oracle's rows for every column
+    count, and Y = alpha A X + beta Y."""
+    import trilinos_amd as ta
+    from oracle import epetra as oe
+    nx, ny, nz = dims
+    n = 3 * nx * ny * nz
+    A = ta.CrsMatrix.galeri(comm, "FlanProxy", nx, ny, nz)
+    assert A.spmm_kernel() == "bsr3"
+    Aor = oe.DistCrs(lambda f, m: oe.flan_proxy_rows(nx, ny, nz, f, m), n, 1)
+    X, _ = oe.epetra_random_mv(29, n, k)
+    Y0, _ = oe.epetra_random_mv(31, n, k)
+    Yd = _upload(ta, comm, Y0)
+    A.apply(_upload(ta, comm, X), Yd, alpha, beta)
+    want = alpha * Aor.apply(X) if beta == 0.0 else alpha * Aor.apply(X) + beta * Y0
+    assert np.array_equal(Yd.download(), want)
+
+
+def test_spmm_bsr3_detects_not_assumes(comm):
+    """Block rows are detected from the CRS: rows whose triple breaks the structure (an entry
+    dropped from one row, a row count not divisible by 3) go to the row kernel, the rest stay
+    blocked -- bit for bit either way; too few qualifying rows and the format is not used."""
+    import trilinos_amd as ta
+    from oracle import epetra as oe
+    nx, ny, nz, k = 9, 8, 7, 4
+    n = 3 * nx * ny * nz - 2                     # last node's triple incomplete
+    rp, gc, vv = oe.flan_proxy_rows(nx, ny, nz, 0, n)
+    keep = np.ones(len(gc), bool)
+    for r in (5, 301, 302, 700):                 # drop each row's 4th entry
+        keep[rp[r] + 3] = False
+    cnt = np.diff(rp) - np.isin(np.arange(n), [5, 301, 302, 700])
+    rp2 = np.concatenate([[0], np.cumsum(cnt)])
+    gc2, vv2 = gc[keep], vv[keep]
+    gc2 = np.where(gc2 < n, gc2, gc2 % n)        # columns of the cut node fold back in range
+    # rows must not repeat a column: rebuild each row unique in insertion order
+    rows = [(gc2[rp2[i]:rp2[i + 1]], vv2[rp2[i]:rp2[i + 1]]) for i in range(n)]
+    rp3, gc3, vv3 = [0], [], []
+    for c, v in rows:
+        _, first = np.unique(c, return_index=True)
+        first = np.sort(first)
+        gc3.extend(c[first].tolist())
+        vv3.extend(v[first].tolist())
+        rp3.append(len(gc3))
+    rp3, gc3, vv3 = np.array(rp3), np.array(gc3), np.array(vv3)
+    A = ta.CrsMatrix(comm, n, rp3, gc3, vv3)
+    assert A.spmm_kernel() == "bsr3"
+    Aor = oe.DistCrs(lambda f, m: (rp3[f:f + m + 1] - rp3[f], gc3[rp3[f]:rp3[f + m]], vv3[rp3[f]:rp3[f + m]]), n, 1)
+    X, _ = oe.epetra_random_mv(37, n, k)
+    Yd = ta.MultiVector(comm, n, k)
+    A.apply(_upload(ta, comm, X), Yd)
+    assert np.array_equal(Yd.download(), Aor.apply(X))

@@ -61,6 +61,8 @@ def _gen(kind, dims):
         return nx * ny, lambda f, m: oe.laplace2d_rows(nx, ny, f, m)
     if kind == "Brick3D":
         return nx * ny * nz, lambda f, m: oe.brick3d_rows(nx, ny, nz, f, m)
+    if kind == "FlanProxy":
+        return 3 * nx * ny * nz, lambda f, m: oe.flan_proxy_rows(nx, ny, nz, f, m)
     from tests.test_plans import random_rows
     n = nx
     return n, lambda f, m: random_rows(n, f, m, 41, per_row=ny)
@@ -70,6 +72,7 @@ def _gen(kind, dims):
                                            ("Laplace3D", (9, 7, 5), 5, 4), ("random", (601, 4, 1), 8, 2),
                                            ("random", (500, 11, 1), 2, 3), ("Brick3D", (9, 8, 7), 8, 3),
                                            ("Brick3D", (10, 8, 9), 8, 3), ("Brick3D", (12, 6, 8), 5, 2),
+                                           ("FlanProxy", (9, 8, 7), 4, 2), ("FlanProxy", (9, 7, 10), 3, 3),
                                            ("random", (700, 0, 1), 4, 2)])
 def test_distributed_spmm_bit_exact(kind, dims, k, P):
     import trilinos_amd as ta

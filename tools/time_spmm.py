@@ -14,7 +14,8 @@ kind, nx, k = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
 jac = len(sys.argv) > 4 and sys.argv[4] == "jacobi"
 reps = int(sys.argv[5]) if len(sys.argv) > 5 else 30
 comm = ta.Comm(0)
-A = ta.CrsMatrix.galeri(comm, kind, nx, nx, nx)
+A = (ta.CrsMatrix.galeri(comm, kind, 81, 81, 80) if kind == "FlanProxy" else  # configs[3]'s shape
+     ta.CrsMatrix.galeri(comm, kind, nx, nx, nx))
 n = A.n_global
 X = ta.MultiVector(comm, n, k)
 X.random(1)

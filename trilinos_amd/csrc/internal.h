@@ -90,6 +90,11 @@ bool launch_spmm_sell(hipStream_t s, int n_local, const long long *off, const in
                       const double *sval, MvDesc X, const double *ghost, long long ldg, MvDesc Y, double alpha,
                       double beta, const int *sel = nullptr, int nsel = 0, double *xr = nullptr,
                       bool xr_ready = false, ColScale cs = {});
+// 3 x 3 block rows (make_bsr3): block rows with len 0 are skipped (left to the row kernel);
+// xr as for launch_spmm_sell (n_local x 8 doubles, filled here for k >= 2).
+void launch_spmm_bsr3(hipStream_t s, int nbr, int n_local, const long long *off, const int *len, const int *bcol,
+                      const double *bval, MvDesc X, MvDesc Y, double alpha, double beta, double *xr,
+                      ColScale cs = {});
 void launch_spmm(hipStream_t s, int row_begin, int row_end, const int *rowptr, const int *cols,
                  const double *vals, MvDesc X, int n_local, const double *ghost, long long ldg,
                  MvDesc Y, double alpha, double beta, const int *sel = nullptr, int nsel = 0, ColScale cs = {});

@@ -297,6 +297,121 @@ bool launch_spmm_sell(hipStream_t s, int n_local, const long long *off, const in
 }
 
 // -------------------------------------------------------------------------------------
+// SpMM x k over 3 x 3 blocks (plan: make_bsr3, plan.cpp; rows in node triples with whole
+// column triples, e.g. 3-dof finite elements): one thread per block row (3 rows), SELL-64 by
+// block, so per block ONE column id (instead of 9) and one contiguous 3 KC-double operand
+// segment of the row-interleaved X copy (xr, KC >= 2) instead of 3 KC gathers.  Each row adds
+// its three products of a block in column order, blocks in ascending order: the stored order,
+// products v * x, no FMA -- bit-identical to k_spmm_sell.  cs: fused right Jacobi scale.
+// -------------------------------------------------------------------------------------
+template <int KC>
+__global__ __launch_bounds__(256) void k_spmm_bsr3(int nbr, const long long *__restrict__ off,
+                                                   const int *__restrict__ len, const int *__restrict__ bcol,
+                                                   const double *__restrict__ bval, const double *__restrict__ xr,
+                                                   MvDesc X, MvDesc Y, int c0, int kc, double alpha, double beta,
+                                                   const double *__restrict__ cs) {
+#pragma clang fp contract(off)
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= nbr) return;
+  const int L = len[b];
+  if (L == 0) return;  // a block row left to the row kernel
+  const long long o = off[b >> 6];
+  const int lane = b & 63;
+  const int *bc = bcol + o + lane;
+  const double *bv = bval + 9 * o + lane;
+  double s[3][KC];
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int c = 0; c < KC; ++c) s[r][c] = 0.0;
+  const double *x1 = colp(X, c0);  // KC == 1: X's column directly
+  constexpr int J = 2;               // blocks whose loads are in flight together
+  for (int q0 = 0; q0 < L; q0 += J) {
+    int j[J];
+    double v[J][9], x[J][3][KC], sc[J][3];
+#pragma unroll
+    for (int u = 0; u < J; ++u) {
+      const int q = q0 + u < L ? q0 + u : L - 1;
+      j[u] = bc[64LL * q];
+#pragma unroll
+      for (int e = 0; e < 9; ++e) v[u][e] = bv[64LL * (9 * q + e)];
+    }
+#pragma unroll
+    for (int u = 0; u < J; ++u) {
+      if constexpr (KC == 1) {
+#pragma unroll
+        for (int e = 0; e < 3; ++e) x[u][e][0] = x1[j[u] + e];
+      } else {
+        const d2 *xp = (const d2 *)(xr + (long long)j[u] * KC);
+#pragma unroll
+        for (int h = 0; h < 3 * KC / 2; ++h) {
+          const d2 t = xp[h];
+          x[u][(2 * h) / KC][(2 * h) % KC] = t.x;
+          x[u][(2 * h + 1) / KC][(2 * h + 1) % KC] = t.y;
+        }
+      }
+      if (cs) {
+#pragma unroll
+        for (int e = 0; e < 3; ++e) sc[u][e] = cs[j[u] + e];
+      }
+    }
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < J; ++u) {
+      if (q0 + u >= L) break;
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int e = 0; e < 3; ++e)
+#pragma unroll
+          for (int c = 0; c < KC; ++c) {
+            const double xv = cs ? sc[u][e] * x[u][e][c] : x[u][e][c];
+            s[r][c] = s[r][c] + v[u][3 * r + e] * xv;
+          }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+      if (c < kc) {
+        double *yp = colp(Y, c0 + c) + 3 * b + r;
+        if (beta == 0.0)
+          *yp = (alpha == 1.0) ? s[r][c] : alpha * s[r][c];
+        else
+          *yp = alpha * s[r][c] + beta * (*yp);
+      }
+    }
+}
+
+void launch_spmm_bsr3(hipStream_t s, int nbr, int n_local, const long long *off, const int *len, const int *bcol,
+                      const double *bval, MvDesc X, MvDesc Y, double alpha, double beta, double *xr,
+                      ColScale cs) {
+  if (nbr <= 0) return;
+  const int k = Y.ncols;
+  const dim3 grid(cdiv(nbr, 256)), gi(cdiv(n_local, 256));
+  for (int c0 = 0; c0 < k; c0 += 8) {
+    const int kc = (k - c0) < 8 ? (k - c0) : 8;
+    if (kc == 1) {
+      k_spmm_bsr3<1><<<grid, 256, 0, s>>>(nbr, off, len, bcol, bval, nullptr, X, Y, c0, kc, alpha, beta, cs.own);
+    } else {
+#define BSR3_XR(KC)                                                                                             \
+  k_interleave<KC><<<gi, 256, 0, s>>>(X, c0, kc, n_local, xr);                                                \
+  k_spmm_bsr3<KC><<<grid, 256, 0, s>>>(nbr, off, len, bcol, bval, xr, X, Y, c0, kc, alpha, beta, cs.own);
+      if (kc <= 2) {
+        BSR3_XR(2)
+      } else if (kc <= 4) {
+        BSR3_XR(4)
+      } else {
+        BSR3_XR(8)
+      }
+#undef BSR3_XR
+    }
+    LAUNCH_CHECK();
+  }
+}
+
+// -------------------------------------------------------------------------------------
 // SpMM x k over row pairs (plan: make_pair_plan, plan.cpp).  One thread per row pair; every
 // X read is a 16-byte load of an aligned pair of rows shared by both rows of the pair (the
 // 8-byte gathers of k_spmm were instruction-bound: tools/mb_spmm.hip measured 1.35 ms

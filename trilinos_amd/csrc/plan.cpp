@@ -520,6 +520,52 @@ void make_sell64(int n_local, const long long *rowptr, const int *lcols, const d
   }
 }
 
+bool make_bsr3(int n_local, const long long *rowptr, const int *lcols, const double *lvals, Bsr3 &out) {
+  out = Bsr3();
+  const int nbr = n_local / 3;
+  out.nbr = nbr;
+  out.len.assign((size_t)nbr, 0);
+  long long qual_rows = 0;
+  for (int b = 0; b < nbr; ++b) {
+    const int r0 = 3 * b;
+    const long long n0 = rowptr[r0 + 1] - rowptr[r0];
+    bool ok = n0 > 0 && n0 % 3 == 0 && rowptr[r0 + 2] - rowptr[r0 + 1] == n0 && rowptr[r0 + 3] - rowptr[r0 + 2] == n0;
+    for (long long e = 0; ok && e < n0; ++e) {
+      const int c = lcols[rowptr[r0] + e];
+      ok = c < n_local && c == lcols[rowptr[r0 + 1] + e] && c == lcols[rowptr[r0 + 2] + e] &&
+           (e % 3 != 0 || (c % 3 == 0 && c + 2 < n_local)) && (e % 3 == 0 || c == lcols[rowptr[r0] + e - 1] + 1);
+    }
+    if (ok) {
+      out.len[(size_t)b] = (int)(n0 / 3);
+      qual_rows += 3;
+    } else {
+      for (int r = r0; r < r0 + 3; ++r) out.rest.push_back(r);
+    }
+  }
+  for (int r = 3 * nbr; r < n_local; ++r) out.rest.push_back(r);
+  if (qual_rows == 0 || qual_rows * 8 < 7LL * n_local) return false;
+  const int nchunks = (nbr + 63) / 64;
+  out.off.assign((size_t)nchunks + 1, 0);
+  for (int c = 0; c < nchunks; ++c) {
+    int w = 0;
+    for (int b = 64 * c; b < std::min(nbr, 64 * c + 64); ++b) w = std::max(w, out.len[(size_t)b]);
+    out.off[(size_t)c + 1] = out.off[(size_t)c] + (long long)w * 64;
+  }
+  out.bcol.assign((size_t)out.off[(size_t)nchunks], 0);
+  out.vals.assign((size_t)out.off[(size_t)nchunks] * 9, 0.0);
+  for (int b = 0; b < nbr; ++b) {
+    const int c = b >> 6, lane = b & 63;
+    for (int s = 0; s < out.len[(size_t)b]; ++s) {
+      const long long slot = out.off[(size_t)c] + 64LL * s;
+      out.bcol[(size_t)(slot + lane)] = lcols[rowptr[3 * b] + 3 * s];
+      for (int r = 0; r < 3; ++r)
+        for (int e = 0; e < 3; ++e)
+          out.vals[(size_t)(9 * slot + 64 * (3 * r + e) + lane)] = lvals[rowptr[3 * b + r] + 3 * s + e];
+    }
+  }
+  return true;
+}
+
 bool make_stencil_groups(const PairTemplates &pt, StencilGroups &out) {
   out = StencilGroups();
   std::vector<int> offs;

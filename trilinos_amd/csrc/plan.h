@@ -70,6 +70,26 @@ struct Sell64 {
 };
 void make_sell64(int n_local, const long long *rowptr, const int *lcols, const double *lvals, Sell64 &out);
 
+// 3 x 3 block form of a CRS whose rows come in triples with one column set made of whole
+// aligned column triples (3 unknowns per mesh node, as in SuiteSparse Flan_1565), DETECTED
+// from the local CRS -- nothing is assumed: block row b = rows 3b .. 3b + 2 qualifies when the
+// three rows have identical sorted column lists consisting of complete triples 3j, 3j + 1,
+// 3j + 2 of owned columns.  Qualifying block rows are stored SELL-64 by block: slot s of the
+// 64 block rows of a chunk at off[chunk] + 64 s + lane holds the block's first column 3j in
+// bcol and its 9 values (row-major: row r, column e at 9 (off[chunk] + 64 s) + 64 (3 r + e)
+// + lane) in vals; len[b] = the block row's blocks (0 for a block row that does not qualify).
+// rest lists the rows of non-qualifying block rows (and a last partial triple) for the
+// row kernel.  Returns false when fewer than 7/8 of the rows qualify (format not used).
+struct Bsr3 {
+  int nbr = 0;
+  std::vector<long long> off;  // nchunks + 1, in block slots
+  std::vector<int> len;        // nbr
+  std::vector<int> bcol;
+  std::vector<double> vals;
+  std::vector<int> rest;
+};
+bool make_bsr3(int n_local, const long long *rowptr, const int *lcols, const double *lvals, Bsr3 &out);
+
 // Row-pair templates for k_spmm_tpl (kernels.hip): a compressed form of the pair plan for
 // matrices whose row pairs repeat a small number of shapes (stencils: the interior pairs of
 // a 7- or 27-point operator are all alike, boundary pairs add a few dozen variants).  A

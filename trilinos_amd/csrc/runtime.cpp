@@ -707,7 +707,8 @@ void mv_assign(const migmres_mv &A, migmres_mv &Y) {
 // ------------------------------------------------------------------------------------
 migmres_crs::~migmres_crs() {
   for (void *p : {(void *)d_soff, (void *)d_slen, (void *)d_scol, (void *)d_sval, (void *)d_xr, (void *)d_tpl_id,
-                  (void *)d_tpl_rec, (void *)d_tpl_val, (void *)d_tpl_rest, (void *)d_tpl3_grp})
+                  (void *)d_tpl_rec, (void *)d_tpl_val, (void *)d_tpl_rest, (void *)d_tpl3_grp, (void *)d_b3off,
+                  (void *)d_b3len, (void *)d_b3col, (void *)d_b3val, (void *)d_b3rest})
     if (p) hipFree(p);
   for (void *p : {(void *)d_export_grp, (void *)d_remote_grp, (void *)d_recv})
     if (p) hipFree(p);
@@ -895,9 +896,33 @@ static void crs_finish(migmres_crs *A, const long long *rowptr, std::vector<int>
           MIG_HIP(hipMemcpy(A->d_sval, sp.vals.data(), sizeof(double) * sp.vals.size(), hipMemcpyHostToDevice));
         }
         A->use_sell = true;
+        // 3 x 3 block rows detected from the CRS (3-dof meshes): one column id per block and
+        // contiguous operand segments; MIGMRES_NO_BSR3=1 keeps the row kernel for every row
+        const char *nb3 = std::getenv("MIGMRES_NO_BSR3");
+        Bsr3 b3;
+        if (!(nb3 && nb3[0] == '1') && make_bsr3(n_local, rowptr, lcols.data(), lvals.data(), b3)) {
+          MIG_HIP(hipMalloc(&A->d_b3off, sizeof(long long) * b3.off.size()));
+          MIG_HIP(hipMalloc(&A->d_b3len, sizeof(int) * (b3.len.size() + 1)));
+          MIG_HIP(hipMalloc(&A->d_b3col, sizeof(int) * (b3.bcol.size() + 1)));
+          MIG_HIP(hipMalloc(&A->d_b3val, sizeof(double) * (b3.vals.size() + 1)));
+          MIG_HIP(hipMemcpy(A->d_b3off, b3.off.data(), sizeof(long long) * b3.off.size(), hipMemcpyHostToDevice));
+          MIG_HIP(hipMemcpy(A->d_b3len, b3.len.data(), sizeof(int) * b3.len.size(), hipMemcpyHostToDevice));
+          MIG_HIP(hipMemcpy(A->d_b3col, b3.bcol.data(), sizeof(int) * b3.bcol.size(), hipMemcpyHostToDevice));
+          MIG_HIP(hipMemcpy(A->d_b3val, b3.vals.data(), sizeof(double) * b3.vals.size(), hipMemcpyHostToDevice));
+          if (!b3.rest.empty()) {
+            MIG_HIP(hipMalloc(&A->d_b3rest, sizeof(int) * b3.rest.size()));
+            MIG_HIP(hipMemcpy(A->d_b3rest, b3.rest.data(), sizeof(int) * b3.rest.size(), hipMemcpyHostToDevice));
+          }
+          A->b3_nbr = b3.nbr;
+          A->n_b3rest = (int)b3.rest.size();
+          double rest_bytes = 0.0;
+          for (int r : b3.rest) rest_bytes += 12.0 * (double)(rowptr[r + 1] - rowptr[r]) + 4.0;
+          A->b3_fixed_bytes = 8.0 * b3.vals.size() + 4.0 * b3.bcol.size() + 4.0 * b3.len.size() + rest_bytes;
+          A->use_bsr3 = true;
+        }
       }
     }
-    A->spmm_fixed_bytes = 12.0 * nnz + 4.0 * (n_local + 1);
+    A->spmm_fixed_bytes = A->use_bsr3 ? A->b3_fixed_bytes : 12.0 * nnz + 4.0 * (n_local + 1);
     {
       // row-pair templates: the pairs' shapes repeat (stencils) -> one byte per pair
       const char *nt = std::getenv("MIGMRES_NO_TPL_SPMM");
@@ -1018,8 +1043,8 @@ static void crs_apply_impl(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, d
     return !(e && e[0] == '1');
   }();
   double *xr = nullptr;
-  if (A.use_sell && !A.use_pairs && !A.use_tpl && sell_xr && k >= 2 && A.n_local > 0 &&
-      (k <= 4 || A.nnz >= 48LL * A.n_local)) {
+  if (A.use_sell && !A.use_pairs && !A.use_tpl && A.n_local > 0 && k >= 2 &&
+      (A.use_bsr3 || (sell_xr && (k <= 4 || A.nnz >= 48LL * A.n_local)))) {
     if (!A.d_xr) MIG_HIP(hipMalloc(&A.d_xr, sizeof(double) * 8 * (size_t)A.n_local));
     xr = A.d_xr;
   }
@@ -1083,6 +1108,14 @@ static void crs_apply_impl(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, d
                       A.tpl_nvals, X.desc(), Y.desc(), alpha, beta, cs.own, A.tpl_slabs, A.tpl_kc);
     if (halo) MIG_HIP(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
     if (A.n_tpl_rest > 0) spmm(A.d_tpl_rest, A.n_tpl_rest);
+  } else if (A.use_bsr3) {
+    // block rows (none reads a ghost column) while the halo is in flight, then the rows left
+    // to the row kernel; the block launch leaves X interleaved for them (one chunk, k <= 8)
+    launch_spmm_bsr3(c->stream, A.b3_nbr, A.n_local, A.d_b3off, A.d_b3len, A.d_b3col, A.d_b3val, X.desc(), Y.desc(),
+                     alpha, beta, xr, cs);
+    xr_ready = xr != nullptr && k <= 8;
+    if (halo) MIG_HIP(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
+    if (A.n_b3rest > 0) spmm(A.d_b3rest, A.n_b3rest);
   } else if (halo && A.d_sel_int) {
     // interior rows while the halo is in flight, then the rows that read ghost columns
     spmm(A.d_sel_int, A.n_sel_int);
@@ -1151,7 +1184,8 @@ void prec_import_ghost_scale(migmres_prec &M) {
 extern "C" int migmres_crs_spmm_kernel(const migmres_crs *A, int *kind) {
   return guard([&] {
     MIG_CHECK(A && kind, "bad arguments");
-    *kind = A->use_tpl3 ? MIGMRES_SPMM_TPL3
+    *kind = A->use_bsr3 ? MIGMRES_SPMM_BSR3
+            : A->use_tpl3 ? MIGMRES_SPMM_TPL3
             : A->use_tpl ? MIGMRES_SPMM_TPL
             : A->use_pairs ? MIGMRES_SPMM_PAIR
             : A->use_sell  ? MIGMRES_SPMM_SELL

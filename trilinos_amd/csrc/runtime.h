@@ -148,7 +148,14 @@ struct migmres_crs {
   int *d_slen = nullptr, *d_scol = nullptr;
   double *d_sval = nullptr;
   bool use_sell = false;
-  double *d_xr = nullptr;  // SELL: row-interleaved copy of X's owned rows (n_local x 8), on first apply with k >= 2
+  double *d_xr = nullptr;
+  // 3 x 3 block rows (make_bsr3) next to the SELL copy, which keeps the rest rows
+  long long *d_b3off = nullptr;
+  int *d_b3len = nullptr, *d_b3col = nullptr, *d_b3rest = nullptr;
+  double *d_b3val = nullptr;
+  int b3_nbr = 0, n_b3rest = 0;
+  double b3_fixed_bytes = 0.0;
+  bool use_bsr3 = false;  // SELL: row-interleaved copy of X's owned rows (n_local x 8), on first apply with k >= 2
   // row-pair templates (k_spmm_tpl) when the pairs repeat a few shapes: templated pairs run
   // there (reading no ghost column, they also make the interior half of the halo overlap);
   // the rest -- pairs that read a ghost column -- go to the kernel above through

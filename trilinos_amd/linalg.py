@@ -180,7 +180,7 @@ class CrsMatrix:
         (migmres_crs_spmm_kernel)."""
         v = C.c_int()
         call("migmres_crs_spmm_kernel", self.h, C.byref(v))
-        return ("csr", "pair", "sell", "tpl", "tpl3")[v.value]
+        return ("csr", "pair", "sell", "tpl", "tpl3", "bsr3")[v.value]
 
     def colmap(self):
         out = np.empty(self.n_cols, dtype=np.int64)
