@@ -304,7 +304,7 @@ bool launch_spmm_sell(hipStream_t s, int n_local, const long long *off, const in
 // its three products of a block in column order, blocks in ascending order: the stored order,
 // products v * x, no FMA -- bit-identical to k_spmm_sell.  cs: fused right Jacobi scale.
 // -------------------------------------------------------------------------------------
-template <int KC>
+template <int KC, int J>
 __global__ __launch_bounds__(256) void k_spmm_bsr3(int nbr, const long long *__restrict__ off,
                                                    const int *__restrict__ len, const int *__restrict__ bcol,
                                                    const double *__restrict__ bval, const double *__restrict__ xr,
@@ -325,7 +325,7 @@ __global__ __launch_bounds__(256) void k_spmm_bsr3(int nbr, const long long *__r
 #pragma unroll
     for (int c = 0; c < KC; ++c) s[r][c] = 0.0;
   const double *x1 = colp(X, c0);  // KC == 1: X's column directly
-  constexpr int J = 2;               // blocks whose loads are in flight together
+  // J blocks' loads in flight together
   for (int q0 = 0; q0 < L; q0 += J) {
     int j[J];
     double v[J][9], x[J][3][KC], sc[J][3];
@@ -388,16 +388,25 @@ void launch_spmm_bsr3(hipStream_t s, int nbr, int n_local, const long long *off,
                       const double *bval, MvDesc X, MvDesc Y, double alpha, double beta, double *xr,
                       ColScale cs) {
   if (nbr <= 0) return;
+  static const int jsel = [] {
+    const char *e = std::getenv("MIGMRES_BSR3_J");
+    return e ? std::atoi(e) : 2;
+  }();
   const int k = Y.ncols;
   const dim3 grid(cdiv(nbr, 256)), gi(cdiv(n_local, 256));
   for (int c0 = 0; c0 < k; c0 += 8) {
     const int kc = (k - c0) < 8 ? (k - c0) : 8;
     if (kc == 1) {
-      k_spmm_bsr3<1><<<grid, 256, 0, s>>>(nbr, off, len, bcol, bval, nullptr, X, Y, c0, kc, alpha, beta, cs.own);
+      k_spmm_bsr3<1, 4><<<grid, 256, 0, s>>>(nbr, off, len, bcol, bval, nullptr, X, Y, c0, kc, alpha, beta, cs.own);
     } else {
 #define BSR3_XR(KC)                                                                                             \
   k_interleave<KC><<<gi, 256, 0, s>>>(X, c0, kc, n_local, xr);                                                \
-  k_spmm_bsr3<KC><<<grid, 256, 0, s>>>(nbr, off, len, bcol, bval, xr, X, Y, c0, kc, alpha, beta, cs.own);
+  if (jsel == 4 && KC <= 4)                                                                                     \
+    k_spmm_bsr3<KC, 4><<<grid, 256, 0, s>>>(nbr, off, len, bcol, bval, xr, X, Y, c0, kc, alpha, beta, cs.own); \
+  else if (jsel == 1)                                                                                           \
+    k_spmm_bsr3<KC, 1><<<grid, 256, 0, s>>>(nbr, off, len, bcol, bval, xr, X, Y, c0, kc, alpha, beta, cs.own); \
+  else                                                                                                          \
+    k_spmm_bsr3<KC, 2><<<grid, 256, 0, s>>>(nbr, off, len, bcol, bval, xr, X, Y, c0, kc, alpha, beta, cs.own);
       if (kc <= 2) {
         BSR3_XR(2)
       } else if (kc <= 4) {
