@@ -789,7 +789,161 @@ __global__ __launch_bounds__(NT) void k_nn_tn_w(MvDesc Q, int L, const double *_
   }
 }
 
+// -------------------------------------------------------------------------------------
+// k > 8 (<= 16), L <= 256: the fused update + projection with each wave owning ROWS instead of
+// a share of the K (projection) dimension, so phase 1 needs no cross-wave reduction and a
+// chunk costs two barriers instead of four.  The workgroup stages a 16-row chunk of Q and X
+// (all L + 16 columns) in LDS with coalesced 16-byte loads (128 B per column) and keeps the
+// next chunk's loads in flight in registers; wave w then takes rows 4w .. 4w + 3 alone:
+//   phase 1: D1 (4 rows x 16) = Q(rows, :) C1 on v_mfma_f64_4x4x4f64 with the four blocks as
+//            the four 4-column groups of X: A = Q(rows, 4s .. 4s + 3) (the same for every
+//            block: broadcast LDS reads), B = C1(4s .. 4s + 3, 4b .. 4b + 3) from LDS;
+//   X1 = X - D1 in the D layout, which is the B layout phase 2 needs (lane 16 m + 4 b + n
+//            holds (row m, column 4 b + n) in both) -- X1 never leaves the registers;
+//   phase 2: acc[t] += Q(rows, 4t .. 4t + 3)^T X1, one 4 x 16 accumulator per 4-column group
+//            of Q (L / 4 doubles per lane).
+// The four waves' accumulators are summed in a fixed order at the end: one L x k partial per
+// workgroup, the layout of k_nn_tn_w's single-launch form.  Read-only (k > 8 never stores X1).
+// LDS: img[16][LDQ] (LDQ = 4 mod 32 doubles: both phases' A reads are conflict-free) and
+// C1s[L / 4][64].
+// -------------------------------------------------------------------------------------
+static constexpr int pw_ldq(int LT) { return ((LT + 16 - 4 + 31) / 32) * 32 + 4; }
+static size_t pw_lds_bytes(int LT) {
+  const size_t img = (size_t)16 * pw_ldq(LT), c1 = (size_t)(LT / 4) * 64;
+  const size_t red = (size_t)(LT / 4) * 64;  // the final reduction reuses img (img >= red)
+  return sizeof(double) * ((img > red ? img : red) + c1);
+}
+
+template <int LT>
+__global__ __launch_bounds__(256) void k_nn_tn_pw(MvDesc Q, int L, const double *__restrict__ C1, int ldc,
+                                                  MvDesc X, int k, int nrows, double *__restrict__ partial,
+                                                  double *__restrict__ sink) {
+  constexpr int NA = LT / 4, LDQ = pw_ldq(LT), LX = LT + 16, NLD = (LX + 31) / 32;
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  double *img = sm;
+  double *C1s = sm + ((size_t)16 * LDQ > (size_t)NA * 64 ? (size_t)16 * LDQ : (size_t)NA * 64);
+  const int t = threadIdx.x, w = t >> 6, l = t & 63;
+  // C1 in the B layout: lane 16 kk + 4 b + n of step s holds C1[4 s + kk][4 b + n] = [.][l & 15]
+  for (int e = t; e < NA * 64; e += 256) {
+    const int s = e >> 6, ll = e & 63, i = 4 * s + (ll >> 4), j = ll & 15;
+    C1s[e] = (i < L && j < k) ? C1[i + (long long)j * ldc] : 0.0;
+  }
+  // columns L .. LT - 1 of the image (Q padding) and the X columns past k stay zero
+  for (int e = t; e < 16 * LDQ; e += 256) img[e] = 0.0;
+  __syncthreads();
+  // loader: image column lcol + 32 m (Q for < L, X column c - LT for LT <= c < LT + k),
+  // rows lrow, lrow + 1 of the chunk: 8 lanes = one 128-B line per column
+  const int lrow = 2 * (t & 7), lcol = t >> 3;
+  const double *lsrc[NLD];
+  int ldst[NLD];
+  bool lon[NLD];
+#pragma unroll
+  for (int m = 0; m < NLD; ++m) {
+    const int c = lcol + 32 * m;
+    lon[m] = c < L || (c >= LT && c < LT + k);
+    const int cc = !lon[m] ? 0 : c;
+    lsrc[m] = (cc < LT ? colp_(Q, cc) : colp_(X, cc - LT)) + lrow;
+    ldst[m] = lrow * LDQ + c;
+  }
+  const long long nchunks = (nrows + 15) / 16;
+  const long long c0 = nchunks * blockIdx.x / gridDim.x, c1 = nchunks * (blockIdx.x + 1) / gridDim.x;
+  double acc[NA];
+#pragma unroll
+  for (int a = 0; a < NA; ++a) acc[a] = 0.0;
+  const int r0 = 4 * w;
+  const int am = l & 3, ak = l >> 4;  // A operand: row m = l & 3, K index = l >> 4
+  d2 p[NLD];
+  if (c0 < c1) {
+#pragma unroll
+    for (int m = 0; m < NLD; ++m) p[m] = *(const d2 *)(lsrc[m] + c0 * 16);
+  }
+  for (long long ch = c0; ch < c1; ++ch) {
+    lds_barrier();  // every wave is done with the previous chunk's image
+#pragma unroll
+    for (int m = 0; m < NLD; ++m) {
+      if (lon[m]) {
+        img[ldst[m]] = p[m].x;
+        img[ldst[m] + LDQ] = p[m].y;
+      }
+    }
+    {
+      const long long nx = ch + 1 < c1 ? ch + 1 : ch;
+#pragma unroll
+      for (int m = 0; m < NLD; ++m) p[m] = *(const d2 *)(lsrc[m] + nx * 16);
+    }
+    lds_barrier();  // image published
+    // phase 1: D1 = Q(rows r0 .. r0 + 3, :) C1
+    double d1 = 0.0;
+    const double *arow = img + (r0 + am) * LDQ + ak;
+#pragma unroll
+    for (int s = 0; s < NA; ++s) d1 = mfma4(arow[4 * s], C1s[s * 64 + l], d1);
+    // X1 (row r0 + (l >> 4), column l & 15), in place in the B layout of phase 2
+    const double x1 = img[(r0 + (l >> 4)) * LDQ + LT + (l & 15)] - d1;
+    // phase 2: acc[t] += Q(rows, 4t .. 4t + 3)^T X1
+    const double *a2 = img + (r0 + ak) * LDQ + am;
+#pragma unroll
+    for (int a = 0; a < NA; ++a) acc[a] = mfma4(a2[4 * a], x1, acc[a]);
+  }
+  // fixed-order sum of the four waves' partials: ((w0 + w1) + w2) + w3
+  double *red = img;
+  for (int q = 0; q < 4; ++q) {
+    lds_barrier();
+    if (w == q) {
+#pragma unroll
+      for (int a = 0; a < NA; ++a) {
+        double v = acc[a];
+        if (q > 0) v = red[a * 64 + l] + v;
+        red[a * 64 + l] = v;
+      }
+    }
+  }
+  lds_barrier();
+  // partial (L x k, column-major) of this workgroup: red[a][lane 16 m + 4 b + n] = C2[4a + m][4b + n]
+  double *out = partial + (long long)blockIdx.x * L * k;
+  for (int e = t; e < NA * 64; e += 256) {
+    const int a = e >> 6, ll = e & 63, i = 4 * a + (ll >> 4), j = ll & 15;
+    if (i < L && j < k) out[i + (long long)j * L] = red[e];
+  }
+  (void)sink;
+}
+
 typedef void (*nt_kernel_t)(MvDesc, int, const double *, int, MvDesc, int, int, double *, double *);
+
+static bool pw_mode() {
+  static int m = -1;
+  if (m < 0) {
+    const char *e = std::getenv("MIGMRES_NT_PW");
+    m = e ? std::atoi(e) : 1;
+  }
+  return m != 0;
+}
+// the per-wave-rows form: k > 8, 64 <= L <= 256
+static bool pw_ok(int L, int k) { return pw_mode() && k > 8 && k <= 16 && L >= 16 && L <= 256; }
+static nt_kernel_t pw_pick(int L) {
+  switch ((L + 15) >> 4) {
+#define PW_CASE(N) \
+  case N:          \
+    return k_nn_tn_pw<16 * N>;
+    PW_CASE(1) PW_CASE(2) PW_CASE(3) PW_CASE(4) PW_CASE(5) PW_CASE(6) PW_CASE(7) PW_CASE(8)
+    PW_CASE(9) PW_CASE(10) PW_CASE(11) PW_CASE(12) PW_CASE(13) PW_CASE(14) PW_CASE(15) PW_CASE(16)
+#undef PW_CASE
+    default: return nullptr;
+  }
+}
+static int pw_per_cu(int L) {
+  static int cache[17] = {};
+  const int n = (L + 15) >> 4;
+  int &v = cache[n];
+  if (!v) {
+    int per_cu = 0;
+    const nt_kernel_t f = pw_pick(L);
+    if (hipFuncSetAttribute((const void *)f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, 256, pw_lds_bytes(16 * n)) != hipSuccess)
+      per_cu = 1;
+    v = per_cu < 1 ? 1 : per_cu > 4 ? 4 : per_cu;
+  }
+  return v;
+}
 
 template <int NJ, bool ST>
 static nt_kernel_t nt_pick_nm(int L) {
@@ -909,7 +1063,7 @@ static bool nw_ok(int L, int k) {
   if (k > 8) return k <= 16 && (nw_single16(L, k) || nw_ok(L, 8));  // all columns, or halves in one launch
   return L >= 64 && L + k <= 512 && nw_wg_per_cu(L, k) >= 1;
 }
-bool nn_tn_paired(int L, int k) { return k > 8 && !nw_single16(L, k); }
+bool nn_tn_paired(int L, int k) { return k > 8 && !pw_ok(L, k) && !nw_single16(L, k); }
 
 static int cu_count() {
   static int cus = 0;
@@ -923,6 +1077,12 @@ static int cu_count() {
 }
 
 int nn_tn_blocks(int nrows, int L, int k) {
+  if (pw_ok(L, k)) {
+    const long long nchunks = (nrows + 15) / 16;
+    long long b = (long long)pw_per_cu(L) * cu_count();
+    if (b > nchunks) b = nchunks;
+    return b < 1 ? 1 : (int)b;
+  }
   if (nw_ok(L, k)) {
     const int kh = k > 8 ? 8 : k;
     const int rw = nw_rw(L, k);
@@ -948,13 +1108,24 @@ int nn_tn_blocks(int nrows, int L, int k) {
   return b < 1 ? 1 : (int)b;
 }
 
-bool nn_tn_supported(int L, int k) { return L >= 1 && k >= 1 && k <= 16 && (L <= NT_MAXL || nw_ok(L, k)); }
+bool nn_tn_supported(int L, int k) {
+  return L >= 1 && k >= 1 && k <= 16 && (L <= NT_MAXL || nw_ok(L, k) || pw_ok(L, k));
+}
 
 void launch_nn_tn(hipStream_t s, MvDesc Q, int L, const double *C1, int ldc, MvDesc X, int nrows,
                   double *partial, int nblocks, double *sink, bool store_x1) {
   const int k = X.ncols;
   if (!nn_tn_supported(L, k))
     throw Error(MIGMRES_EINVAL, "nn_tn: 1 <= k <= 16 and L <= 256 (L + k <= 512 for k <= 8, L >= 64)");
+  if (pw_ok(L, k)) {
+    if (store_x1) throw Error(MIGMRES_EINVAL, "nn_tn: k > 8 is read-only");
+    const int LT = 16 * ((L + 15) >> 4);
+    pw_per_cu(L);  // raises the kernel's dynamic LDS limit
+    hipLaunchKernelGGL(pw_pick(L), dim3(nblocks), dim3(256), pw_lds_bytes(LT), s, Q, L, C1, ldc, X, k, nrows,
+                       partial, sink);
+    LAUNCH_CHECK_();
+    return;
+  }
 
   if (nw_ok(L, k)) {
     const bool paired = nn_tn_paired(L, k);
