@@ -872,17 +872,67 @@ __global__ __launch_bounds__(256) void k_nn_tn_pw(MvDesc Q, int L, const double 
       for (int m = 0; m < NLD; ++m) p[m] = *(const d2 *)(lsrc[m] + nx * 16);
     }
     lds_barrier();  // image published
-    // phase 1: D1 = Q(rows r0 .. r0 + 3, :) C1
-    double d1 = 0.0;
+    // Both phases in batches of BT K steps whose LDS operands are read one batch ahead (the
+    // compiler, left to itself, kept 2-4 reads in flight and each MFMA waited out the LDS
+    // latency).  The empty asm statements keep each batch's reads above the previous batch's
+    // MFMAs.
+    constexpr int BT = 6;
+    // phase 1: D1 = Q(rows r0 .. r0 + 3, :) C1 in two interleaved accumulator chains
+    double d1q[2] = {0.0, 0.0};
     const double *arow = img + (r0 + am) * LDQ + ak;
+    {
+      double ca[BT], cb[BT], na[BT], nb[BT];
 #pragma unroll
-    for (int s = 0; s < NA; ++s) d1 = mfma4(arow[4 * s], C1s[s * 64 + l], d1);
+      for (int j = 0; j < BT; ++j) {
+        ca[j] = j < NA ? arow[4 * j] : 0.0;
+        cb[j] = j < NA ? C1s[j * 64 + l] : 0.0;
+      }
+#pragma unroll
+      for (int s0 = 0; s0 < NA; s0 += BT) {
+#pragma unroll
+        for (int j = 0; j < BT; ++j) {
+          const int s = s0 + BT + j;
+          na[j] = s < NA ? arow[4 * s] : 0.0;
+          nb[j] = s < NA ? C1s[s * 64 + l] : 0.0;
+        }
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int j = 0; j < BT; ++j)
+          if (s0 + j < NA) d1q[j & 1] = mfma4(ca[j], cb[j], d1q[j & 1]);
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int j = 0; j < BT; ++j) {
+          ca[j] = na[j];
+          cb[j] = nb[j];
+        }
+      }
+    }
+    const double d1 = d1q[0] + d1q[1];
     // X1 (row r0 + (l >> 4), column l & 15), in place in the B layout of phase 2
     const double x1 = img[(r0 + (l >> 4)) * LDQ + LT + (l & 15)] - d1;
     // phase 2: acc[t] += Q(rows, 4t .. 4t + 3)^T X1
     const double *a2 = img + (r0 + ak) * LDQ + am;
+    {
+      constexpr int B2 = 2 * BT;
+      double ca[B2], na[B2];
 #pragma unroll
-    for (int a = 0; a < NA; ++a) acc[a] = mfma4(a2[4 * a], x1, acc[a]);
+      for (int j = 0; j < B2; ++j) ca[j] = j < NA ? a2[4 * j] : 0.0;
+#pragma unroll
+      for (int a0 = 0; a0 < NA; a0 += B2) {
+#pragma unroll
+        for (int j = 0; j < B2; ++j) {
+          const int a = a0 + B2 + j;
+          na[j] = a < NA ? a2[4 * a] : 0.0;
+        }
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int j = 0; j < B2; ++j)
+          if (a0 + j < NA) acc[a0 + j] = mfma4(ca[j], x1, acc[a0 + j]);
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int j = 0; j < B2; ++j) ca[j] = na[j];
+      }
+    }
   }
   // fixed-order sum of the four waves' partials: ((w0 + w1) + w2) + w3
   double *red = img;
@@ -909,16 +959,24 @@ __global__ __launch_bounds__(256) void k_nn_tn_pw(MvDesc Q, int L, const double 
 
 typedef void (*nt_kernel_t)(MvDesc, int, const double *, int, MvDesc, int, int, double *, double *);
 
-static bool pw_mode() {
+static int pw_mode() {
   static int m = -1;
   if (m < 0) {
     const char *e = std::getenv("MIGMRES_NT_PW");
     m = e ? std::atoi(e) : 1;
   }
-  return m != 0;
+  return m;
 }
-// the per-wave-rows form: k > 8, 64 <= L <= 256
-static bool pw_ok(int L, int k) { return pw_mode() && k > 8 && k <= 16 && L >= 16 && L <= 256; }
+// The per-wave-rows form for k > 8: measured against k_nn_tn_w at 256^3, k = 16 (tools/mb_k16.cpp,
+// same box): L = 64 4.55 vs 3.97 TB/s, L = 128 4.25 vs 4.09, but L = 160 .. 208 4.0 vs 4.2-4.4 and
+// L = 256 3.9 vs 4.0 -- every form of this kernel (barriers, accumulator chains, LDS read depth)
+// sits near 30 TF/s of fp64 MFMA, which is where the chip holds its clock down under this load
+// (MI355X_MICROARCH.md 'DVFS give-back').  So by default (MIGMRES_NT_PW=1) L <= 144, which also
+// replaces the narrow k_nn_tn for L < 64 at k > 8; 2: up to L = 256; 0: off.
+static bool pw_ok(int L, int k) {
+  const int m = pw_mode();
+  return m != 0 && k > 8 && k <= 16 && L >= 16 && L <= (m >= 2 ? 256 : 144);
+}
 static nt_kernel_t pw_pick(int L) {
   switch ((L + 15) >> 4) {
 #define PW_CASE(N) \
