@@ -967,15 +967,17 @@ static int pw_mode() {
   }
   return m;
 }
-// The per-wave-rows form for k > 8: measured against k_nn_tn_w at 256^3, k = 16 (tools/mb_k16.cpp,
-// same box): L = 64 4.55 vs 3.97 TB/s, L = 128 4.25 vs 4.09, but L = 160 .. 208 4.0 vs 4.2-4.4 and
-// L = 256 3.9 vs 4.0 -- every form of this kernel (barriers, accumulator chains, LDS read depth)
-// sits near 30 TF/s of fp64 MFMA, which is where the chip holds its clock down under this load
-// (MI355X_MICROARCH.md 'DVFS give-back').  So by default (MIGMRES_NT_PW=1) L <= 144, which also
-// replaces the narrow k_nn_tn for L < 64 at k > 8; 2: up to L = 256; 0: off.
+// The per-wave-rows form for k > 8, measured against the kernels it replaces at 256^3, k = 16
+// (tools/mb_k16.cpp, same box, profiles/r3m_k16_nn_tn_sweep.txt): L = 16 0.85 vs 2.02 ms (the
+// narrow k_nn_tn ran below L = 64), 32 1.37 vs 2.13, 48 1.82 vs 2.85, 64 2.36 vs 2.60, 96 3.46 vs
+// 3.59; from L = 128 on k_nn_tn_w is ahead (4.51 vs 4.58 ms, L = 192 6.08 vs 6.81).  Every form
+// of the phase structure tried (this one without the cross-wave reduction, two accumulator
+// chains, LDS operands read a batch ahead) stays near 4.0-4.6 TB/s = 30 TF/s of fp64 MFMA at
+// L >= 160 with the clock at 2.0-2.3 GHz under this load (GRBM_GUI_ACTIVE, r3m).  Default
+// (MIGMRES_NT_PW=1) L <= 112; 2: up to L = 256; 0: off.
 static bool pw_ok(int L, int k) {
   const int m = pw_mode();
-  return m != 0 && k > 8 && k <= 16 && L >= 16 && L <= (m >= 2 ? 256 : 144);
+  return m != 0 && k > 8 && k <= 16 && L >= 16 && L <= (m >= 2 ? 256 : 112);
 }
 static nt_kernel_t pw_pick(int L) {
   switch ((L + 15) >> 4) {
