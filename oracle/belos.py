@@ -819,6 +819,7 @@ DEFAULTS = {   # BelosBlockGmresSolMgr.hpp:317-335
     "Orthogonalization": "DGKS", "Flexible Gmres": False, "Explicit Residual Test": False,
     "Implicit Residual Scaling": "Norm of Preconditioned Initial Residual",
     "Explicit Residual Scaling": "Norm of Initial Residual",
+    "Orthogonalization Constant": -1.0,
 }
 
 
@@ -837,6 +838,8 @@ class BlockGmresSolMgr:
         elif p["Orthogonalization"] == "DGKS":
             from .dgks import DGKS
             self.ortho = DGKS()
+            if p["Orthogonalization Constant"] > 0:   # setDepTol(orthoKappa) (BelosBlockGmresSolMgr.hpp:607-625)
+                self.ortho.dep_tol = float(p["Orthogonalization Constant"])
         else:
             raise ValueError("oracle supports ICGS and DGKS")
 

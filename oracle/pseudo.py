@@ -23,6 +23,7 @@ DEFAULTS = {   # BelosPseudoBlockGmresSolMgr.hpp:494-507
     "Explicit Residual Test": False,
     "Implicit Residual Scaling": "Norm of Preconditioned Initial Residual",
     "Explicit Residual Scaling": "Norm of Initial Residual",
+    "Orthogonalization Constant": -1.0,
 }
 
 
@@ -117,6 +118,8 @@ class PseudoBlockGmresSolMgr:
         elif p["Orthogonalization"] == "DGKS":
             from .dgks import DGKS
             self.ortho = DGKS()
+            if p["Orthogonalization Constant"] > 0:   # setDepTol(orthoKappa) (BelosPseudoBlockGmresSolMgr.hpp:736-754)
+                self.ortho.dep_tol = float(p["Orthogonalization Constant"])
         else:
             raise ValueError("oracle supports ICGS and DGKS")
 

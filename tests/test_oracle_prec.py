@@ -189,3 +189,18 @@ def test_pseudo_block_deflation():
         assert rel.max() <= 1e-9
         if q == 1:
             assert r["deflations"] >= 1
+
+
+def test_oracle_orthogonalization_constant():
+    """"Orthogonalization Constant" > 0 with DGKS is the ortho manager's dep_tol
+    (BelosBlockGmresSolMgr.hpp:607-625, BelosPseudoBlockGmresSolMgr.hpp:736-754); <= 0 or ICGS
+    leave the defaults."""
+    import math
+    from oracle import belos as ob, pseudo as op
+    for cls in (ob.BlockGmresSolMgr, op.PseudoBlockGmresSolMgr):
+        assert cls(None, {"Orthogonalization": "DGKS", "Orthogonalization Constant": 0.3}).ortho.dep_tol == 0.3
+        assert cls(None, {"Orthogonalization": "DGKS"}).ortho.dep_tol == 1 / math.sqrt(2)
+        assert cls(None, {"Orthogonalization": "DGKS", "Orthogonalization Constant": 0.0}).ortho.dep_tol == \
+            1 / math.sqrt(2)
+        assert not hasattr(cls(None, {"Orthogonalization": "ICGS", "Orthogonalization Constant": 0.3}).ortho,
+                           "dep_tol")

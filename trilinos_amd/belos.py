@@ -201,10 +201,14 @@ class LinearProblem:
 
 
 _INT_PARAMS = {"Block Size", "Num Blocks", "Maximum Iterations", "Maximum Restarts", "Verbosity",
-               "Output Frequency", "Deflation Quorum"}
-_BOOL_PARAMS = {"Adaptive Block Size", "Flexible Gmres", "Explicit Residual Test"}
-_DOUBLE_PARAMS = {"Convergence Tolerance"}
-_STRING_PARAMS = {"Orthogonalization", "Implicit Residual Scaling", "Explicit Residual Scaling"}
+               "Output Frequency", "Deflation Quorum", "Output Style"}
+_BOOL_PARAMS = {"Adaptive Block Size", "Flexible Gmres", "Explicit Residual Test",
+                "Show Maximum Residual Norm Only"}
+_DOUBLE_PARAMS = {"Convergence Tolerance", "Orthogonalization Constant"}
+_STRING_PARAMS = {"Orthogonalization", "Implicit Residual Scaling", "Explicit Residual Scaling", "Timer Label"}
+
+# Belos::OutputType (BelosTypes.hpp): "Output Style" takes either the enum or its int
+General, Brief = 0, 1
 
 # BelosBlockGmresSolMgr.hpp:317-338, 438-486 and DefaultSolverParameters::convTol
 DEFAULT_PARAMETERS = {
@@ -214,6 +218,10 @@ DEFAULT_PARAMETERS = {
     "Explicit Residual Test": False,
     "Implicit Residual Scaling": "Norm of Preconditioned Initial Residual",
     "Explicit Residual Scaling": "Norm of Initial Residual",
+    # recorded and reported; the device path writes no status output (BelosBlockGmresSolMgr.hpp:459-486)
+    "Output Style": General, "Show Maximum Residual Norm Only": False, "Timer Label": "Belos",
+    # > 0 with "DGKS": the ortho manager's dep_tol (BelosBlockGmresSolMgr.hpp:607-625)
+    "Orthogonalization Constant": -1.0,
 }
 SCALE_TYPES = ("Norm of Initial Residual", "Norm of Preconditioned Initial Residual", "Norm of RHS", "None")
 
@@ -387,6 +395,8 @@ PSEUDO_DEFAULT_PARAMETERS = {
     "Deflation Quorum": 1, "Orthogonalization": "ICGS", "Explicit Residual Test": False,
     "Implicit Residual Scaling": "Norm of Preconditioned Initial Residual",
     "Explicit Residual Scaling": "Norm of Initial Residual",
+    "Output Style": General, "Show Maximum Residual Norm Only": False, "Timer Label": "Belos",
+    "Orthogonalization Constant": -1.0,
 }
 
 

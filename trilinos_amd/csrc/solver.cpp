@@ -590,7 +590,8 @@ struct FastIcgs {
     // second projection of a column that kept >= dep_tol of its norm (:1094-1119), i.e. in
     // rounding, with the same dependency test newDot < blk_tol oldDot (:1204-1210) that the
     // Gram form takes on its pivots.  MIGMRES_FB_GRAM_DGKS=0 keeps DGKS on the column passes.
-    return gram_on && (!slow->dgks || gram_dgks) && slow->steps == 2 && k >= 2 && L >= 1 && L <= 1024 &&
+    // A non-default "Orthogonalization Constant" keeps DGKS on the column passes.
+    return gram_on && (!slow->dgks || (gram_dgks && slow->dep_tol == 1.0 / std::sqrt(2.0))) && slow->steps == 2 && k >= 2 && L >= 1 && L <= 1024 &&
            ((k <= 8 && L * k <= 7680) || (k > 8 && k <= 16));
   }
   bool gram_dgks = [] {
@@ -847,6 +848,13 @@ struct Params {
   std::string exp_scale = "Norm of Initial Residual";
   int verbosity = 0;
   int output_freq = -1;
+  // recorded and reported, no effect on the device path (BelosBlockGmresSolMgr.hpp:459-486)
+  std::string timer_label = "Belos";
+  int output_style = 0;  // Belos::General
+  bool show_max_res_norm_only = false;
+  // "Orthogonalization Constant": DGKS's dep_tol when > 0 (BelosBlockGmresSolMgr.hpp:607-625)
+  double ortho_kappa = -1.0;
+  double dgks_dep_tol() const { return ortho_kappa > 0 ? ortho_kappa : 1.0 / std::sqrt(2.0); }
 };
 
 }  // namespace
@@ -1500,6 +1508,7 @@ struct Engine {
       }
       std::vector<double> z0((size_t)block * block, 0.0);
       S->ortho.dgks = S->p.ortho == "DGKS";
+      S->ortho.dep_tol = S->p.dgks_dep_tol();
       if (S->use_fast && S->fast.supports(block)) {
         S->fast.slow = &S->ortho;
         S->fast.setup(lp.X->ctx, lp.X->n_global, lp.X->n_local, block, it.sd);
@@ -1880,6 +1889,7 @@ struct PseudoEngine : Engine {
     bool converged = true;
     S->loa = false;
     S->ortho.dgks = p.ortho == "DGKS";
+    S->ortho.dep_tol = p.dgks_dep_tol();
     PseudoIter it;
     it.nb = p.num_blocks;
     it.V = MvPtr(mv_create(lp.X->ctx, lp.X->n_global, lp.X->n_local, block * (p.num_blocks + 1)));
@@ -2049,6 +2059,10 @@ extern "C" int migmres_solver_set_int(migmres_solver *s, const char *name, long 
       s->p.verbosity = (int)v;
     } else if (n == "Output Frequency") {
       s->p.output_freq = (int)v;
+    } else if (n == "Output Style") {
+      s->p.output_style = (int)v;
+    } else if (n == "Show Maximum Residual Norm Only") {
+      s->p.show_max_res_norm_only = v != 0;
     } else {
       throw Error(MIGMRES_EINVAL, "unknown integer parameter \"" + n + "\"");
     }
@@ -2060,6 +2074,8 @@ extern "C" int migmres_solver_set_double(migmres_solver *s, const char *name, do
     const std::string n(name);
     if (n == "Convergence Tolerance")
       s->p.tol = v;
+    else if (n == "Orthogonalization Constant")
+      s->p.ortho_kappa = v;
     else
       throw Error(MIGMRES_EINVAL, "unknown double parameter \"" + n + "\"");
   });
@@ -2079,6 +2095,8 @@ extern "C" int migmres_solver_set_string(migmres_solver *s, const char *name, co
                     val == "Norm of RHS" || val == "None",
                 "invalid residual scaling type \"" + val + "\"");
       (n[0] == 'I' ? s->p.imp_scale : s->p.exp_scale) = val;
+    } else if (n == "Timer Label") {
+      s->p.timer_label = val;
     } else {
       throw Error(MIGMRES_EINVAL, "unknown string parameter \"" + n + "\"");
     }
@@ -2119,6 +2137,11 @@ std::string param_text(const Params &p) {
   b("Explicit Residual Test", p.exp_res_test);
   line("Implicit Residual Scaling", "string", p.imp_scale);
   line("Explicit Residual Scaling", "string", p.exp_scale);
+  i("Output Style", p.output_style);
+  b("Show Maximum Residual Norm Only", p.show_max_res_norm_only);
+  line("Timer Label", "string", p.timer_label);
+  std::snprintf(num, sizeof num, "%.17g", p.ortho_kappa);
+  line("Orthogonalization Constant", "double", num);
   return out;
 }
 void put_text(const std::string &t, char *buf, int len, int *needed) {
@@ -2161,14 +2184,18 @@ extern "C" int migmres_solver_get_int(const migmres_solver *s, const char *name,
     else if (n == "Explicit Residual Test") *v = p.exp_res_test;
     else if (n == "Verbosity") *v = p.verbosity;
     else if (n == "Output Frequency") *v = p.output_freq;
+    else if (n == "Output Style") *v = p.output_style;
+    else if (n == "Show Maximum Residual Norm Only") *v = p.show_max_res_norm_only;
     else throw Error(MIGMRES_EINVAL, "unknown integer parameter \"" + n + "\"");
   });
 }
 extern "C" int migmres_solver_get_double(const migmres_solver *s, const char *name, double *v) {
   return guard([&] {
     MIG_CHECK(s && name && v, "bad arguments");
-    MIG_CHECK(std::string(name) == "Convergence Tolerance", "unknown double parameter \"" + std::string(name) + "\"");
-    *v = s->p.tol;
+    const std::string n(name);
+    if (n == "Convergence Tolerance") *v = s->p.tol;
+    else if (n == "Orthogonalization Constant") *v = s->p.ortho_kappa;
+    else throw Error(MIGMRES_EINVAL, "unknown double parameter \"" + n + "\"");
   });
 }
 extern "C" int migmres_solver_get_string(const migmres_solver *s, const char *name, char *v, int len) {
@@ -2178,6 +2205,7 @@ extern "C" int migmres_solver_get_string(const migmres_solver *s, const char *na
     const std::string &val = n == "Orthogonalization" ? s->p.ortho
                              : n == "Implicit Residual Scaling" ? s->p.imp_scale
                              : n == "Explicit Residual Scaling" ? s->p.exp_scale
+                             : n == "Timer Label" ? s->p.timer_label
                              : throw Error(MIGMRES_EINVAL, "unknown string parameter \"" + n + "\"");
     put_text(val, v, len, nullptr);
   });
