@@ -257,11 +257,42 @@ int migmres_dgks_normalize(migmres_mv *X, double *B, int ldb, int *rank);
  * inverse diagonal as compute() :1240-1270).  A must outlive the preconditioner. */
 int migmres_jacobi_create(migmres_crs *A, int sweeps, double damping, migmres_prec **out);
 int migmres_prec_destroy(migmres_prec *M);
-/* Y = M X (Ifpack2::Relaxation::apply, alpha = 1, beta = 0).  X may alias Y (apply(x, x)):
- * the sweeps then read a deep copy of X, as Ifpack2_Relaxation_def.hpp:539-551. */
+/* Y = M X (Ifpack2::Relaxation::apply / Ifpack2::Chebyshev::apply, alpha = 1, beta = 0).
+ * X may alias Y (apply(x, x)): M then reads a deep copy of X, as
+ * Ifpack2_Relaxation_def.hpp:539-551 and Ifpack2_Chebyshev_def.hpp:456-473 do.  A Chebyshev
+ * preconditioner with zero_starting_solution = 0 starts from Y's current contents. */
 int migmres_prec_apply(migmres_prec *M, const migmres_mv *X, migmres_mv *Y);
 /* The stored inverse diagonal (n_local doubles). */
 int migmres_prec_diagonal(const migmres_prec *M, double *dinv_out);
+
+/* Chebyshev polynomial smoother (Ifpack2::Chebyshev, ifpack2/src/Ifpack2_Chebyshev_def.hpp
+ * over Ifpack2_Details_Chebyshev_def.hpp): the parameter list of Details::Chebyshev
+ * (:280-300 defaults, setParameters :333-677) as plain fields.  max_eigenvalue NaN = not
+ * given (estimate it: the power method on D^-1 A, :1341-1473, from an Epetra MINSTD random
+ * vector with `seed` -- Tpetra's randomize() stream is not reproduced).  compute() (:739-896)
+ * runs inside create; apply is migmres_prec_apply (ifpackApplyImpl :1221-1339, or
+ * textbookApplyImpl :1163-1208 with textbook != 0). */
+typedef struct migmres_chebyshev_params {
+  int degree;                 /* "chebyshev: degree" (1) */
+  double max_eigenvalue;      /* "chebyshev: max eigenvalue" (NaN = estimate) */
+  double ratio_eigenvalue;    /* "chebyshev: ratio eigenvalue" (30, >= 1) */
+  double boost_factor;        /* "chebyshev: boost factor" (1.1, >= 1) */
+  double min_diagonal_value;  /* "chebyshev: min diagonal value" (eps) */
+  int eigenvalue_max_iterations; /* "chebyshev: eigenvalue max iterations" (10) */
+  int zero_starting_solution; /* "chebyshev: zero starting solution" (1) */
+  int assume_matrix_unchanged; /* "chebyshev: assume matrix does not change" (0) */
+  int textbook_algorithm;     /* "chebyshev: textbook algorithm" (0) */
+  unsigned int seed;          /* power-method start vector stream (1) */
+} migmres_chebyshev_params;
+/* Fill *p with the reference defaults. */
+int migmres_chebyshev_params_default(migmres_chebyshev_params *p);
+/* Chebyshev preconditioner on A (A must outlive it).  Errors as setParameters' checks:
+ * degree < 0, ratio < 1, boost < 1, a non-finite max eigenvalue or min diagonal value. */
+int migmres_chebyshev_create(migmres_crs *A, const migmres_chebyshev_params *p, migmres_prec **out);
+/* The eigenvalue bounds apply() uses (getLambdaMaxForApply) and the power method's estimate
+ * (NaN when it did not run). */
+int migmres_chebyshev_lambdas(const migmres_prec *M, double *lambda_max_for_apply, double *lambda_min_for_apply,
+                              double *computed_lambda_max);
 
 /* ---------------- solver manager (Belos::BlockGmresSolMgr) ---------------- */
 

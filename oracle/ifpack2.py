@@ -61,3 +61,157 @@ class Jacobi:
             R = X - self.A(Y)
             Y = 1.0 * Y + ab * R
         return Y
+
+
+# ---------------------------------------------------------------------------------------
+# Ifpack2::Chebyshev (ifpack2/src/Ifpack2_Chebyshev_def.hpp over
+# Ifpack2_Details_Chebyshev_def.hpp), the smoother of SURVEY 8(f) rank 2.
+#   parameters (Details::Chebyshev :280-300 defaults, setParameters :333-677): "chebyshev:
+#     degree" 1, "chebyshev: max eigenvalue" / "min eigenvalue" (unset = estimate), "ratio
+#     eigenvalue" 30, "boost factor" 1.1, "min diagonal value" eps, "eigenvalue max
+#     iterations" 10, "zero starting solution" true, "textbook algorithm" false;
+#   compute() (:739-896): D^-1 by reciprocal_threshold (:95-187: |d| < minVal -> minVal, else
+#     1/d -- the reference stores minVal itself, not its reciprocal), the power method on
+#     D^-1 A (:1341-1473) unless "assume matrix does not change" with estimates in hand, then
+#     lambdaMin = lambdaMax / eigRatio and Ifpack's lambdaMax ~ 1 special case (:884-895);
+#   apply() (:909-957): ifpackApplyImpl (:1221-1339) or textbookApplyImpl (:1163-1208), the
+#     ChebyshevKernel expression W = beta W + (alpha d_i)(b - A x), X += W
+#     (Ifpack2_Details_ChebyshevKernel_def.hpp:160-169, 472-480).
+# The power method's initial vector: Tpetra's randomize() stream is not restated; both sides
+# use Epetra's MINSTD stream from a seed (oracle.epetra.epetra_random_mv), so the estimate is
+# pinned only to this restatement ("parity unpinned" against Tpetra's generator).
+# ---------------------------------------------------------------------------------------
+
+CHEBYSHEV_DEFAULTS = {
+    "chebyshev: degree": 1,
+    "chebyshev: ratio eigenvalue": 30.0,
+    "chebyshev: boost factor": 1.1,
+    "chebyshev: min diagonal value": float(np.finfo(np.float64).eps),
+    "chebyshev: eigenvalue max iterations": 10,
+    "chebyshev: zero starting solution": True,
+    "chebyshev: assume matrix does not change": False,
+    "chebyshev: textbook algorithm": False,
+}
+
+
+def reciprocal_threshold(d, min_val):
+    """LocalReciprocalThreshold (Ifpack2_Details_Chebyshev_def.hpp:104-115)."""
+    d = np.asarray(d, dtype=np.float64)
+    with np.errstate(divide="ignore"):
+        inv = 1.0 / d
+    return np.where(np.abs(d) < abs(min_val), min_val, inv)
+
+
+class Chebyshev:
+    """Y = M X for Ifpack2::Chebyshev; `A` applies the operator to an (n, k) array, `diag` is
+    the diagonal copy, `dot(a, b)` / `norm(a)` are the global inner product and 2-norm."""
+
+    def __init__(self, A, diag, params=None, seed=1, dot=None, norm=None):
+        p = dict(CHEBYSHEV_DEFAULTS)
+        p.update(params or {})
+        self.p = p
+        self.A = A
+        self.seed = seed
+        self.dot = dot or (lambda a, b: float(np.dot(a, b)))
+        self.norm = norm or (lambda a: float(np.sqrt(np.dot(a, a))))
+        self.user_lmax = p.get("chebyshev: max eigenvalue", np.nan)
+        self.eig_ratio = float(p["chebyshev: ratio eigenvalue"])
+        self.boost = float(p["chebyshev: boost factor"])
+        self.degree = int(p["chebyshev: degree"])
+        self.dinv = reciprocal_threshold(diag, float(p["chebyshev: min diagonal value"]))
+        self.computed_lmax = np.nan
+        self.n_apply = 0
+        self.compute()
+
+    def power_method(self, x):
+        """powerMethodWithInitGuess (:1344-1406)."""
+        lam = 0.0
+        nrm = self.norm(x)
+        if nrm == 0.0:
+            raise RuntimeError("power method initial guess has zero norm")
+        x = (1.0 / nrm) * x
+        for _ in range(int(self.p["chebyshev: eigenvalue max iterations"])):
+            y = self.A(x[:, None])[:, 0]
+            y = (1.0 * self.dinv) * y
+            lam = self.dot(y, x) / self.dot(x, x)
+            nrm = self.norm(y)
+            if nrm == 0.0:
+                return 0.0
+            x = (1.0 / nrm) * y
+        return lam
+
+    def compute(self):
+        from oracle.epetra import epetra_random_mv
+        n = self.dinv.shape[0]
+        if not self.p["chebyshev: assume matrix does not change"] or \
+                (np.isnan(self.computed_lmax) and np.isnan(self.user_lmax)):
+            x, _ = epetra_random_mv(self.seed, n, 1)
+            lam = self.power_method(x[:, 0].copy())
+            if lam < 0.0:   # powerMethod (:1457-1471): retry once from |x|
+                x, _ = epetra_random_mv(self.seed, n, 1)
+                lam = self.power_method(np.abs(x[:, 0]))
+            self.computed_lmax = lam
+        lmax = self.computed_lmax if np.isnan(self.user_lmax) else float(self.user_lmax)
+        lmin = lmax / self.eig_ratio
+        ratio = self.eig_ratio
+        if not self.p["chebyshev: textbook algorithm"] and abs(lmax - 1.0) < 1.0e-6:
+            lmin = lmax = ratio = 1.0
+        self.lmax, self.lmin, self.ratio = lmax, lmin, ratio
+
+    def __call__(self, B, X0=None):
+        """Ifpack2::Chebyshev::apply(B, X): X = M B (zero start) or the polynomial step from X0."""
+        self.n_apply += 1
+        B = np.asarray(B, dtype=np.float64)
+        X = np.zeros_like(B) if X0 is None else np.array(X0, dtype=np.float64)
+        d = self.dinv[:, None]
+        if self.p["chebyshev: textbook algorithm"]:
+            return self._textbook(B, X, d)
+        if self.degree <= 0:
+            return X
+        lmax, lmin, ratio = self.lmax, self.lmin, self.ratio
+        if lmin == 1.0 and lmax == lmin:          # :1250-1253
+            return (1.0 * d) * B
+        alpha = lmax / ratio
+        beta = self.boost * lmax
+        delta = 2.0 / (beta - alpha)
+        theta = (beta + alpha) / 2.0
+        s1 = theta * delta
+        zero = self.p["chebyshev: zero starting solution"]
+        if zero:
+            W = ((1.0 / theta) * d) * B
+            X = W.copy()
+        else:
+            W = ((1.0 / theta) * d) * (B - self.A(X))
+            X = X + W
+        rhok = 1.0 / s1
+        for _ in range(1, self.degree):
+            rhokp1 = 1.0 / (2.0 * s1 - rhok)
+            dtemp1 = rhokp1 * rhok
+            dtemp2 = 2.0 * rhokp1 * delta
+            rhok = rhokp1
+            W = dtemp1 * W + (dtemp2 * d) * (B - self.A(X))
+            X = X + W
+        return X
+
+    def _textbook(self, B, X, d):
+        """textbookApplyImpl (:1163-1208)."""
+        lmax = self.lmax
+        lmin = lmax / self.ratio
+        dd = (lmax + lmin) / 2.0
+        c = (lmax - lmin) / 2.0
+        if self.p["chebyshev: zero starting solution"] and self.degree > 0:
+            X = np.zeros_like(B)
+        P = None
+        alpha = 0.0
+        for i in range(self.degree):
+            R = B - self.A(X)
+            Z = (1.0 * d) * R
+            if i == 0:
+                P = Z.copy()
+                alpha = 2.0 / dd
+            else:
+                beta = alpha * (c / 2.0) * (c / 2.0)
+                alpha = 1.0 / (dd - beta)
+                P = Z + beta * P
+            X = X + alpha * P
+        return X

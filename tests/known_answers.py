@@ -129,3 +129,31 @@ def transpose_apply(rowptr, lcols, vals, X, ncols):
 
 DIAG_TEST_PARAMS = {"Block Size": 1, "Num Blocks": 10, "Maximum Iterations": 100, "Maximum Restarts": 10,
                     "Convergence Tolerance": 1.0e-10}
+
+
+def laplace1d_rows(n_global):
+    """Ifpack2_UnitTestChebyshev2.cpp:384-416: row 0 (2, -1), middle rows (-1, 2, -1), last
+    row (-1, 2), in that insertion order."""
+    def gen(first, m):
+        rp, gc, vv = [0], [], []
+        for g in range(first, first + m):
+            if g == 0:
+                cols, vals = [0, 1], [2.0, -1.0]
+            elif g == n_global - 1:
+                cols, vals = [g - 1, g], [-1.0, 2.0]
+            else:
+                cols, vals = [g - 1, g, g + 1], [-1.0, 2.0, -1.0]
+            gc += cols
+            vv += vals
+            rp.append(len(gc))
+        return np.asarray(rp, dtype=np.int64), np.asarray(gc, dtype=np.int64), np.asarray(vv)
+    return gen
+
+
+def laplace1d_lambda_max(n):
+    """Demmel's bound the reference test sets as "chebyshev: max eigenvalue" (:424-426)."""
+    return 2.0 * (1.0 - np.cos((np.pi * n) / (n + 1.0)))
+
+
+# Ifpack2_UnitTestChebyshev2.cpp:312-314: degree 50, 15 (then 30) power iterations, 10000 rows
+CHEB2_ROWS, CHEB2_DEGREE, CHEB2_EIG_ITERS = 10000, 50, 15

@@ -1,0 +1,251 @@
+"""Ifpack2::Chebyshev on the device against oracle/ifpack2.py Chebyshev.
+
+* Known answers of Ifpack2_UnitTestChebyshev.cpp Test0 (diag(2): degree 1 exact, 0.5; degree
+  4 within 1e-4), one GPU and loopback ranks.
+* With "chebyshev: max eigenvalue" given, apply() is elementwise work plus the bit-exact SpMM,
+  so the device result equals the oracle's bit for bit: Ifpack and textbook variants, zero
+  and nonzero start, several degrees, 1..3 ranks.
+* The power method's estimate (device dots vs numpy dots) agrees to 1e-13 relative, and so
+  does the apply that uses it.
+* Ifpack2_UnitTestChebyshev2.cpp Convergence on the device: Ifpack's variant is no worse than
+  the textbook one after the 30-iteration estimate (:754-771).
+* Right-preconditioned Block GMRES with the device Chebyshev follows the oracle solve
+  (iterations, counters, history).
+"""
+
+import numpy as np
+import pytest
+
+from tests.known_answers import (CHEB2_DEGREE, CHEB2_EIG_ITERS, CHEB2_ROWS, ifpack2_test_matrix_rows,
+                                 laplace1d_lambda_max, laplace1d_rows)
+from tests.parity import hist_close
+from tests.test_gpu_loopback import run_ranks
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def comm():
+    import torch
+    assert torch.cuda.is_available()
+    import trilinos_amd as ta
+    return ta.Comm(device=0)
+
+
+def _device_apply(comm, gen, n, B, params, X0=None, seed=1):
+    import trilinos_amd as ta
+    first, nloc = ta.uniform_map(n, comm.nranks, comm.rank)
+    rp, gc, vv = gen(first, nloc)
+    A = ta.CrsMatrix(comm, n, rp, gc, vv)
+    M = ta.Chebyshev(A, seed=seed)
+    M.setParameters(params)
+    M.initialize()
+    M.compute()
+    k = B.shape[1]
+    Bd, Xd = ta.MultiVector(comm, n, k), ta.MultiVector(comm, n, k)
+    Bd.upload(B[first:first + nloc])
+    if X0 is None:
+        Xd.put_scalar(0.0)
+    else:
+        Xd.upload(X0[first:first + nloc])
+    M.apply(Bd, Xd)
+    return first, Xd.download(), M.getLambdaMaxForApply(), M.getComputedLambdaMax()
+
+
+def _oracle(gen, n, params, seed=1):
+    from oracle import epetra as oe
+    from oracle.ifpack2 import Chebyshev, crs_diagonal_fast
+    A = oe.DistCrs(gen, n, 1)
+    rp, gc, vv = gen(0, n)
+    return A, Chebyshev(A.apply, crs_diagonal_fast(rp, gc, vv, 0, n), params, seed=seed)
+
+
+TEST0 = {"chebyshev: degree": 1, "chebyshev: min eigenvalue": 0.0, "chebyshev: max eigenvalue": 1.0,
+         "chebyshev: ratio eigenvalue": 1.0 / 0.9}
+
+
+def _test0(comm, n):
+    import trilinos_amd as ta
+    gen = ifpack2_test_matrix_rows(n)
+    first, nloc = ta.uniform_map(n, comm.nranks, comm.rank)
+    rp, gc, vv = gen(first, nloc)
+    A = ta.CrsMatrix(comm, n, rp, gc, vv)
+    M = ta.Chebyshev(A)
+    M.setParameters(TEST0)
+    M.initialize()
+    M.compute()
+    x, y = ta.MultiVector(comm, n, 2), ta.MultiVector(comm, n, 2)
+    x.put_scalar(1.0)
+    M.applyMat(x, y)
+    two = y.download()
+    M.apply(x, y)
+    half = y.download()
+    M.setParameters({"chebyshev: degree": 4})
+    M.apply(x, y)
+    half4 = y.download()
+    return nloc, two, half, half4
+
+
+def test_chebyshev_test0_one_gpu(comm):
+    nloc, two, half, half4 = _test0(comm, 5)
+    assert np.array_equal(two, np.full((5, 2), 2.0))
+    np.testing.assert_allclose(half, 0.5, rtol=0, atol=1e-13)
+    np.testing.assert_allclose(half4, 0.5, rtol=0, atol=1e-4)
+
+
+@pytest.mark.parametrize("P", [2, 3])
+def test_chebyshev_test0_ranks(P):
+    """5 rows per process, as the reference test's map."""
+    for nloc, two, half, half4 in run_ranks(P, lambda c: _test0(c, 5 * P)):
+        assert nloc == 5
+        assert np.array_equal(two, np.full((nloc, 2), 2.0))
+        np.testing.assert_allclose(half, 0.5, rtol=0, atol=1e-13)
+        np.testing.assert_allclose(half4, 0.5, rtol=0, atol=1e-4)
+
+
+CASES = [
+    ({"chebyshev: degree": 1}, False),
+    ({"chebyshev: degree": 3}, False),
+    ({"chebyshev: degree": 8, "chebyshev: ratio eigenvalue": 20.0}, False),
+    ({"chebyshev: degree": 8, "chebyshev: boost factor": 1.3}, True),
+    ({"chebyshev: degree": 6, "chebyshev: textbook algorithm": True}, False),
+    ({"chebyshev: degree": 0}, False),
+]
+
+
+def _laplace2d(nx, ny):
+    from oracle import epetra as oe
+    return nx * ny, (lambda f, m: oe.laplace2d_rows(nx, ny, f, m))
+
+
+@pytest.mark.parametrize("case", range(len(CASES)))
+def test_chebyshev_apply_bit_exact_with_given_lambda(comm, case):
+    from oracle import epetra as oe
+    extra, nonzero_start = CASES[case]
+    n, gen = _laplace2d(40, 37)
+    params = dict(extra, **{"chebyshev: max eigenvalue": 1.9})
+    if nonzero_start:
+        params["chebyshev: zero starting solution"] = False
+    B, _ = oe.epetra_random_mv(5, n, 3)
+    X0 = oe.epetra_random_mv(9, n, 3)[0] if nonzero_start else None
+    _, M = _oracle(gen, n, params)
+    want = M(B, X0)
+    _, got, lmax, _ = _device_apply(comm, gen, n, B, params, X0)
+    assert lmax == M.lmax
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("P", [2, 3])
+def test_chebyshev_apply_ranks_bit_exact(P):
+    from oracle import epetra as oe
+    n, gen = _laplace2d(30, 29)
+    params = {"chebyshev: degree": 5, "chebyshev: max eigenvalue": 1.95}
+    B, _ = oe.epetra_random_mv(5, n, 2)
+    _, M = _oracle(gen, n, params)
+    want = M(B)
+    for first, got, _, _ in run_ranks(P, lambda c: _device_apply(c, gen, n, B, params)):
+        assert np.array_equal(got, want[first:first + got.shape[0]])
+
+
+@pytest.mark.parametrize("P", [1, 2])
+def test_chebyshev_power_method_estimate(comm, P):
+    from oracle import epetra as oe
+    n, gen = _laplace2d(50, 41)
+    params = {"chebyshev: degree": 4, "chebyshev: eigenvalue max iterations": 12}
+    B, _ = oe.epetra_random_mv(5, n, 2)
+    _, M = _oracle(gen, n, params, seed=7)
+    want = M(B)
+    run = (lambda fn: [fn(comm)]) if P == 1 else (lambda fn: run_ranks(P, fn))
+    for first, got, lmax, computed in run(lambda c: _device_apply(c, gen, n, B, params, seed=7)):
+        assert abs(computed - M.computed_lmax) <= 1e-13 * M.computed_lmax
+        assert lmax == computed
+        np.testing.assert_allclose(got, want[first:first + got.shape[0]], rtol=1e-11, atol=1e-13)
+
+
+def test_chebyshev2_convergence_on_device(comm):
+    from oracle import epetra as oe
+    n = CHEB2_ROWS
+    gen = laplace1d_rows(n)
+    A = oe.DistCrs(gen, n, 1)
+    xe, _ = oe.epetra_random_mv(3, n, 1)
+    B = A.apply(xe)
+    r0 = np.linalg.norm(B)
+    res = {}
+    for textbook in (False, True):
+        p = {"chebyshev: degree": CHEB2_DEGREE, "chebyshev: eigenvalue max iterations": 2 * CHEB2_EIG_ITERS,
+             "chebyshev: textbook algorithm": textbook}
+        _, X, _, _ = _device_apply(comm, gen, n, B, p)
+        res[textbook] = np.linalg.norm(B - A.apply(X), axis=0).max()
+    assert res[False] < 1e-2 * r0
+    assert not (res[False] > res[True] and abs(res[False] - res[True]) / res[True] > 1e-4), res
+    # with Demmel's lambdaMax (Test 1): both variants reduce the residual
+    for textbook in (False, True):
+        p = {"chebyshev: degree": CHEB2_DEGREE, "chebyshev: max eigenvalue": laplace1d_lambda_max(n),
+             "chebyshev: textbook algorithm": textbook}
+        _, X, _, _ = _device_apply(comm, gen, n, B, p)
+        assert np.linalg.norm(B - A.apply(X)) < 1e-2 * r0
+
+
+def test_chebyshev_apply_alias_alpha_beta(comm):
+    """Ifpack2_Chebyshev_def.hpp:418-495: apply(x, x) reads a copy; alpha folds into X;
+    beta adds beta * Y_orig; alpha = 0 scales Y by beta."""
+    import trilinos_amd as ta
+    from oracle import epetra as oe
+    n, gen = _laplace2d(20, 21)
+    params = {"chebyshev: degree": 3, "chebyshev: max eigenvalue": 1.9}
+    _, Mo = _oracle(gen, n, params)
+    rp, gc, vv = gen(0, n)
+    A = ta.CrsMatrix(comm, n, rp, gc, vv)
+    M = ta.Chebyshev(A)
+    M.setParameters(params)
+    M.compute()
+    B, _ = oe.epetra_random_mv(5, n, 2)
+    Y0, _ = oe.epetra_random_mv(6, n, 2)
+    x = ta.MultiVector(comm, n, 2)
+    x.upload(B)
+    M.apply(x, x)
+    assert np.array_equal(x.download(), Mo(B))
+    x.upload(B)
+    y = ta.MultiVector(comm, n, 2)
+    y.upload(Y0)
+    M.apply(x, y, alpha=2.0, beta=0.5)
+    np.testing.assert_allclose(y.download(), 0.5 * Y0 + Mo(2.0 * B), rtol=1e-14, atol=1e-14)
+    y.upload(Y0)
+    M.apply(x, y, alpha=0.0, beta=3.0)
+    np.testing.assert_allclose(y.download(), 3.0 * Y0, rtol=0, atol=0)
+    with pytest.raises(ValueError):
+        M.setParameters({"chebyshev: ratio eigenvalue": 0.5})
+
+
+@pytest.mark.parametrize("side", ["right", "left"])
+def test_block_gmres_with_chebyshev(comm, side):
+    import trilinos_amd as ta
+    from oracle import belos as ob, epetra as oe
+    from tests.parity import oracle_rerun
+    nx, ny, nz = 14, 13, 12
+    n = nx * ny * nz
+    gen = lambda f, m: oe.laplace3d_rows(nx, ny, nz, f, m)  # noqa: E731
+    cheb = {"chebyshev: degree": 3, "chebyshev: max eigenvalue": 1.95}
+    Aor, Mo = _oracle(gen, n, cheb)
+    Xe, _ = oe.epetra_random_mv(3, n, 4)
+    Bh = Aor.apply(Xe)
+    params = {"Block Size": 4, "Num Blocks": 15, "Maximum Iterations": 300, "Maximum Restarts": 20,
+              "Convergence Tolerance": 1e-9, "Orthogonalization": "ICGS"}
+    ref = ob.solve(Aor.apply, Bh, params, **{side: Mo})
+    A = ta.CrsMatrix.galeri(comm, "Laplace3D", nx, ny, nz)
+    M = ta.Chebyshev(A)
+    M.setParameters(cheb)
+    M.compute()
+    B, X = ta.MultiVector(comm, n, 4), ta.MultiVector(comm, n, 4)
+    B.upload(Bh)
+    X.put_scalar(0.0)
+    lp = ta.LinearProblem(A, X, B)
+    (lp.setRightPrec if side == "right" else lp.setLeftPrec)(M)
+    assert lp.setProblem()
+    sm = ta.BlockGmresSolMgr(lp, params)
+    assert (sm.solve() == ta.Converged) == ref["converged"]
+    assert sm.getNumIters() == ref["iterations"]
+    c = sm.counters()
+    assert c["applies"] == ref["n_apply"] and c["prec_applies"] == ref["n_prec"]
+    hist_close(sm.residualHistory(), ref["history"],
+               oracle_rerun(ob.solve, Aor.apply, Bh, params, **{side: Mo}))

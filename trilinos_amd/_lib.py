@@ -85,6 +85,9 @@ _SIGS = {
     "migmres_prec_destroy": [vp],
     "migmres_prec_apply": [vp, vp, vp],
     "migmres_prec_diagonal": [vp, P(f64)],
+    "migmres_chebyshev_params_default": [vp],
+    "migmres_chebyshev_create": [vp, vp, P(vp)],
+    "migmres_chebyshev_lambdas": [vp, P(f64), P(f64), P(f64)],
     "migmres_solver_create": [vp, P(vp)],
     "migmres_solver_create_named": [vp, C.c_char_p, P(vp)],
     "migmres_solver_set_prec": [vp, i32, vp],

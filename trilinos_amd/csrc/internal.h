@@ -149,6 +149,15 @@ void launch_diag_inv(hipStream_t s, const int *rowptr, const int *cols, const do
                      double *dinv);
 void launch_jacobi(hipStream_t s, MvDesc X, MvDesc Y, const double *dinv, double omega, int nrows,
                    bool accumulate);
+// Ifpack2::Chebyshev: dinv = reciprocal_threshold(diag, min_val); the ChebyshevKernel step
+// W = [beta W +] (alpha dinv) R, X = X + W (xmode 1) / X = W (2) / untouched (0); Y = a A + b B
+// without contraction.
+void launch_diag_recip_threshold(hipStream_t s, const int *rowptr, const int *cols, const double *vals, int n,
+                                 double min_val, double *dinv);
+void launch_cheb_update(hipStream_t s, MvDesc R, MvDesc W, MvDesc X, const double *dinv, double alpha, double beta,
+                        bool use_beta, int xmode, int nrows);
+void launch_lincomb(hipStream_t s, double a, MvDesc A, double b, MvDesc B, MvDesc Y, int nrows);
+void launch_abs(hipStream_t s, MvDesc Y, int nrows);  // Y = |Y| (negative entries negated)
 // Import exchange layout [neighbour][column][count] (grp[i] = (offset, count) of entry i's
 // neighbour group): send[off*k + c*cnt + i-off] = X[lids[i], c]; ghost[c*ldg + i] = recv[...].
 void launch_pack(hipStream_t s, MvDesc X, const int *lids, const int2 *grp, int count, double *send, int k);

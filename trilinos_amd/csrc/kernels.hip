@@ -1553,6 +1553,65 @@ __global__ __launch_bounds__(256) void k_jacobi(MvDesc X, MvDesc Y, const double
   *y = ACC ? 1.0 * (*y) + t : t;
 }
 
+// Ifpack2::Chebyshev's inverse diagonal: reciprocal_threshold of the diagonal copy
+// (Ifpack2_Details_Chebyshev_def.hpp:104-115): |d| < |min_val| stores min_val itself.
+__global__ __launch_bounds__(256) void k_diag_recip_threshold(const int *__restrict__ rowptr,
+                                                              const int *__restrict__ cols,
+                                                              const double *__restrict__ vals, int n,
+                                                              double min_val, double *__restrict__ dinv) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= n) return;
+  double d = 0.0;
+  for (int p = rowptr[r]; p < rowptr[r + 1]; ++p)
+    if (cols[p] == r) {
+      d = vals[p];
+      break;
+    }
+  dinv[r] = fabs(d) < fabs(min_val) ? min_val : 1.0 / d;
+}
+
+// The ChebyshevKernel step (Ifpack2_Details_ChebyshevKernel_def.hpp:160-169, 472-480) on a
+// residual R = B - A X formed by the SpMM: W = beta W + (alpha d_i) R (BETA) or
+// W = (alpha d_i) R, then X = X + W (XMODE 1), X = W (XMODE 2, the zero-start first step)
+// or X untouched (XMODE 0); each product and sum rounded separately.
+template <bool BETA, int XMODE>
+__global__ __launch_bounds__(256) void k_cheb_update(MvDesc R, MvDesc W, MvDesc X, const double *__restrict__ dinv,
+                                                     double alpha, double beta, int nrows) {
+#pragma clang fp contract(off)
+  const int c = blockIdx.y;
+  const long long r = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (r >= nrows) return;
+  const double t = (alpha * dinv[r]) * colp(R, c)[r];
+  double *wp = colp(W, c) + r;
+  const double w = BETA ? beta * (*wp) + t : t;
+  *wp = w;
+  if (XMODE == 1) {
+    double *xp = colp(X, c) + r;
+    *xp = *xp + w;
+  } else if (XMODE == 2) {
+    colp(X, c)[r] = w;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_abs(MvDesc Y, int nrows) {
+  const int c = blockIdx.y;
+  const long long r = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (r >= nrows) return;
+  double *y = colp(Y, c) + r;
+  if (*y < 0.0) *y = -*y;
+}
+
+// Y = a A + b B with each product and the sum rounded separately (KokkosBlas axpby as the
+// textbook Chebyshev's P = Z + beta P and X = X + alpha P evaluate it).
+__global__ __launch_bounds__(256) void k_lincomb(double a, MvDesc A, double b, MvDesc B, MvDesc Y, int nrows) {
+#pragma clang fp contract(off)
+  const int c = blockIdx.y;
+  const long long r = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (r >= nrows) return;
+  const double pa = a * colp(A, c)[r], pb = b * colp(B, c)[r];
+  colp(Y, c)[r] = pa + pb;
+}
+
 __global__ __launch_bounds__(256) void k_scaled_copy(const double *__restrict__ a, double omega, double *out, int n) {
 #pragma clang fp contract(off)
   const long long r = (long long)blockIdx.x * 256 + threadIdx.x;
@@ -1568,6 +1627,37 @@ void launch_diag_inv(hipStream_t s, const int *rowptr, const int *cols, const do
                      double *dinv) {
   if (n <= 0) return;
   k_diag_inv<<<cdiv(n, 256), 256, 0, s>>>(rowptr, cols, vals, n, dinv);
+  LAUNCH_CHECK();
+}
+void launch_diag_recip_threshold(hipStream_t s, const int *rowptr, const int *cols, const double *vals, int n,
+                                 double min_val, double *dinv) {
+  if (n <= 0) return;
+  k_diag_recip_threshold<<<cdiv(n, 256), 256, 0, s>>>(rowptr, cols, vals, n, min_val, dinv);
+  LAUNCH_CHECK();
+}
+void launch_cheb_update(hipStream_t s, MvDesc R, MvDesc W, MvDesc X, const double *dinv, double alpha, double beta,
+                        bool use_beta, int xmode, int nrows) {
+  if (nrows <= 0 || W.ncols <= 0) return;
+  const dim3 g(cdiv(nrows, 256), W.ncols);
+  if (use_beta) {
+    if (xmode == 1) k_cheb_update<true, 1><<<g, 256, 0, s>>>(R, W, X, dinv, alpha, beta, nrows);
+    else if (xmode == 2) k_cheb_update<true, 2><<<g, 256, 0, s>>>(R, W, X, dinv, alpha, beta, nrows);
+    else k_cheb_update<true, 0><<<g, 256, 0, s>>>(R, W, X, dinv, alpha, beta, nrows);
+  } else {
+    if (xmode == 1) k_cheb_update<false, 1><<<g, 256, 0, s>>>(R, W, X, dinv, alpha, beta, nrows);
+    else if (xmode == 2) k_cheb_update<false, 2><<<g, 256, 0, s>>>(R, W, X, dinv, alpha, beta, nrows);
+    else k_cheb_update<false, 0><<<g, 256, 0, s>>>(R, W, X, dinv, alpha, beta, nrows);
+  }
+  LAUNCH_CHECK();
+}
+void launch_abs(hipStream_t s, MvDesc Y, int nrows) {
+  if (nrows <= 0 || Y.ncols <= 0) return;
+  k_abs<<<dim3(cdiv(nrows, 256), Y.ncols), 256, 0, s>>>(Y, nrows);
+  LAUNCH_CHECK();
+}
+void launch_lincomb(hipStream_t s, double a, MvDesc A, double b, MvDesc B, MvDesc Y, int nrows) {
+  if (nrows <= 0 || Y.ncols <= 0) return;
+  k_lincomb<<<dim3(cdiv(nrows, 256), Y.ncols), 256, 0, s>>>(a, A, b, B, Y, nrows);
   LAUNCH_CHECK();
 }
 void launch_jacobi(hipStream_t s, MvDesc X, MvDesc Y, const double *dinv, double omega, int nrows,

@@ -1,7 +1,12 @@
-// Point-Jacobi preconditioner on the device: Ifpack2::Relaxation with "relaxation: type" =
+// Preconditioners on the device: point Jacobi, Ifpack2::Relaxation with "relaxation: type" =
 // "Jacobi" (ifpack2/src/Ifpack2_Relaxation_def.hpp; compute() :990-1270 keeps the
 // reciprocal of the diagonal, ApplyInverseJacobi :1390-1454 applies it), the
-// right/left preconditioner of config 5.
+// right/left preconditioner of config 5; and the
+// Chebyshev smoother, Ifpack2::Chebyshev.
+#include <cmath>
+#include <limits>
+#include <memory>
+
 #include "runtime.h"
 
 using namespace migmres;
@@ -12,6 +17,8 @@ migmres_prec::~migmres_prec() {
   if (d_gsdinv) hipFree(d_gsdinv);
   delete work;
   delete xcopy;
+  delete cheb_w;
+  delete cheb_p;
 }
 
 namespace migmres {
@@ -34,22 +41,150 @@ static bool mv_overlap(const migmres_mv &X, const migmres_mv &Y) {
   return false;
 }
 
-void prec_apply(migmres_prec &M, const migmres_mv &X_in, migmres_mv &Y) {
-  MIG_CHECK(X_in.ncols == Y.ncols, "Jacobi apply: X and Y column counts differ");
-  MIG_CHECK(X_in.n_local == M.A->n_local && Y.n_local == M.A->n_local, "Jacobi apply: row map mismatch");
+// scratch multivector with X's shape, (re)made when the column count changes
+static migmres_mv &scratch(migmres_mv *&w, const migmres_mv &X) {
+  if (!w || w->ncols != X.ncols) {
+    delete w;
+    w = mv_create(X.ctx, X.n_global, X.n_local, X.ncols);
+  }
+  return *w;
+}
+
+// R = B - A X (the Tpetra::Details::residual expression b - sum, by the SpMM with alpha = -1,
+// beta = 1 on a copy of B)
+static void residual(migmres_prec &M, const migmres_mv &B, const migmres_mv &X, migmres_mv &R) {
+  mv_assign(B, R);
+  crs_apply(*M.A, X, R, -1.0, 1.0);
+}
+
+// Ifpack2::Chebyshev::apply: X = M B (Ifpack2_Details_Chebyshev_def.hpp:909-957).
+static void chebyshev_apply(migmres_prec &M, const migmres_mv &B, migmres_mv &X) {
   migmres_ctx *c = M.ctx;
   const int n = M.A->n_local;
-  // X aliasing Y (apply(x, x)): sweep from a deep copy of X, as the reference does
+  const migmres_chebyshev_params &p = M.cheb;
+  const int deg = p.degree;
+  if (p.textbook_algorithm) {  // textbookApplyImpl (:1163-1208)
+    const double lmax = M.cheb_lmax, lmin = lmax / M.cheb_ratio;
+    const double d = (lmax + lmin) / 2.0, cc = (lmax - lmin) / 2.0;
+    if (p.zero_starting_solution && deg > 0) mv_init(X, 0.0);
+    migmres_mv &R = scratch(M.work, B), &P = scratch(M.cheb_p, B), &Z = scratch(M.cheb_w, B);
+    double alpha = 0.0;
+    for (int i = 0; i < deg; ++i) {
+      residual(M, B, X, R);
+      ProfScope ps(c, K_AXPBY, 8.0 * n * (6.0 * B.ncols + 1.0));
+      launch_jacobi(c->stream, R.desc(), Z.desc(), M.d_dinv, 1.0, n, false);  // Z = D^-1 R
+      if (i == 0) {
+        mv_assign(Z, P);
+        alpha = 2.0 / d;
+      } else {
+        const double beta = alpha * (cc / 2.0) * (cc / 2.0);
+        alpha = 1.0 / (d - beta);
+        launch_lincomb(c->stream, 1.0, Z.desc(), beta, P.desc(), P.desc(), n);  // P = Z + beta P
+      }
+      launch_lincomb(c->stream, alpha, P.desc(), 1.0, X.desc(), X.desc(), n);  // X = X + alpha P
+    }
+    return;
+  }
+  if (deg <= 0) return;  // ifpackApplyImpl (:1221-1339)
+  if (M.cheb_lmin == 1.0 && M.cheb_lmax == M.cheb_lmin) {  // A = I: X = D^-1 B (:1250-1253)
+    ProfScope ps(c, K_AXPBY, 8.0 * n * (2.0 * B.ncols + 1.0));
+    launch_jacobi(c->stream, B.desc(), X.desc(), M.d_dinv, 1.0, n, false);
+    return;
+  }
+  const double alpha = M.cheb_lmax / M.cheb_ratio;
+  const double beta = p.boost_factor * M.cheb_lmax;
+  const double delta = 2.0 / (beta - alpha);
+  const double theta = (beta + alpha) / 2.0;
+  const double s1 = theta * delta;
+  migmres_mv &W = scratch(M.cheb_w, B);
+  if (p.zero_starting_solution) {  // W = (1/theta) D^-1 B, X = W
+    ProfScope ps(c, K_AXPBY, 8.0 * n * (3.0 * B.ncols + 1.0));
+    launch_cheb_update(c->stream, B.desc(), W.desc(), X.desc(), M.d_dinv, 1.0 / theta, 0.0, false, 2, n);
+  } else {  // W = (1/theta) D^-1 (B - A X), X += W
+    migmres_mv &R = scratch(M.work, B);
+    residual(M, B, X, R);
+    ProfScope ps(c, K_AXPBY, 8.0 * n * (5.0 * B.ncols + 1.0));
+    launch_cheb_update(c->stream, R.desc(), W.desc(), X.desc(), M.d_dinv, 1.0 / theta, 0.0, false, 1, n);
+  }
+  double rhok = 1.0 / s1;
+  for (int k = 1; k < deg; ++k) {
+    const double rhokp1 = 1.0 / (2.0 * s1 - rhok);
+    const double dtemp1 = rhokp1 * rhok;
+    const double dtemp2 = 2.0 * rhokp1 * delta;
+    rhok = rhokp1;
+    migmres_mv &R = scratch(M.work, B);
+    residual(M, B, X, R);
+    ProfScope ps(c, K_AXPBY, 8.0 * n * (6.0 * B.ncols + 1.0));
+    launch_cheb_update(c->stream, R.desc(), W.desc(), X.desc(), M.d_dinv, dtemp2, dtemp1, true, 1, n);
+  }
+}
+
+// powerMethodWithInitGuess (Ifpack2_Details_Chebyshev_def.hpp:1344-1406) on D^-1 A.
+static double power_method(migmres_prec &M, migmres_mv &x, migmres_mv &y) {
+  migmres_ctx *c = M.ctx;
+  const int n = M.A->n_local;
+  double nrm = 0.0, top = 0.0, bottom = 0.0, lambda = 0.0;
+  mv_norm(x, &nrm, 2);
+  MIG_CHECK(nrm != 0.0, "Ifpack2::Chebyshev::powerMethodWithInitGuess: the initial guess has zero norm");
+  mv_scale(x, 1.0 / nrm);
+  for (int it = 0; it < M.cheb.eigenvalue_max_iterations; ++it) {
+    crs_apply(*M.A, x, y, 1.0, 0.0);
+    launch_jacobi(c->stream, y.desc(), y.desc(), M.d_dinv, 1.0, n, false);  // y = D^-1 y
+    mv_dot(y, x, &top);
+    mv_dot(x, x, &bottom);
+    lambda = top / bottom;
+    mv_norm(y, &nrm, 2);
+    if (nrm == 0.0) return 0.0;
+    mv_assign(y, x);
+    mv_scale(x, 1.0 / nrm);
+  }
+  return lambda;
+}
+
+// compute() (Ifpack2_Details_Chebyshev_def.hpp:739-896) after the inverse diagonal.
+static void chebyshev_compute(migmres_prec &M) {
+  const migmres_chebyshev_params &p = M.cheb;
+  if (!p.assume_matrix_unchanged || (std::isnan(M.cheb_computed_lmax) && std::isnan(p.max_eigenvalue))) {
+    std::unique_ptr<migmres_mv> x(mv_create(M.ctx, M.A->n_global, M.A->n_local, 1));
+    std::unique_ptr<migmres_mv> y(mv_create(M.ctx, M.A->n_global, M.A->n_local, 1));
+    unsigned seed = p.seed;
+    mv_random(*x, &seed);
+    double lmax = power_method(M, *x, *y);
+    if (lmax < 0.0) {  // powerMethod (:1457-1471): once more from |random|
+      seed = p.seed;
+      mv_random(*x, &seed);
+      launch_abs(M.ctx->stream, x->desc(), M.A->n_local);  // PositivizeVector (:191-221)
+      lmax = power_method(M, *x, *y);
+    }
+    M.cheb_computed_lmax = lmax;
+  }
+  M.cheb_lmax = std::isnan(p.max_eigenvalue) ? M.cheb_computed_lmax : p.max_eigenvalue;
+  M.cheb_lmin = M.cheb_lmax / p.ratio_eigenvalue;
+  M.cheb_ratio = p.ratio_eigenvalue;
+  if (!p.textbook_algorithm && std::fabs(M.cheb_lmax - 1.0) < 1.0e-6) {  // Ifpack's lambdaMax ~ 1 case
+    M.cheb_lmin = 1.0;
+    M.cheb_lmax = 1.0;
+    M.cheb_ratio = 1.0;
+  }
+}
+
+void prec_apply(migmres_prec &M, const migmres_mv &X_in, migmres_mv &Y) {
+  MIG_CHECK(X_in.ncols == Y.ncols, "preconditioner apply: X and Y column counts differ");
+  MIG_CHECK(X_in.n_local == M.A->n_local && Y.n_local == M.A->n_local, "preconditioner apply: row map mismatch");
+  migmres_ctx *c = M.ctx;
+  const int n = M.A->n_local;
+  // X aliasing Y (apply(x, x)): work from a deep copy of X, as the reference does
   const migmres_mv *Xp = &X_in;
   if (mv_overlap(X_in, Y)) {
-    if (!M.xcopy || M.xcopy->ncols != X_in.ncols) {
-      delete M.xcopy;
-      M.xcopy = mv_create(c, X_in.n_global, X_in.n_local, X_in.ncols);
-    }
-    mv_assign(X_in, *M.xcopy);
+    mv_assign(X_in, scratch(M.xcopy, X_in));
     Xp = M.xcopy;
   }
   const migmres_mv &X = *Xp;
+  if (M.kind == 1) {
+    chebyshev_apply(M, X, Y);
+    ++M.n_apply;
+    return;
+  }
   {
     ProfScope ps(c, K_AXPBY, 8.0 * n * (2.0 * X.ncols + 1.0));
     launch_jacobi(c->stream, X.desc(), Y.desc(), M.d_dinv, M.damping, n, false);
@@ -91,6 +226,60 @@ extern "C" int migmres_jacobi_create(migmres_crs *A, int sweeps, double damping,
     MIG_HIP(hipStreamSynchronize(A->ctx->stream));
     if (sweeps == 1) prec_import_ghost_scale(*M);  // the fused form's ghost column scale
     *out = M;
+  });
+}
+
+extern "C" int migmres_chebyshev_params_default(migmres_chebyshev_params *p) {
+  return guard([&] {
+    MIG_CHECK(p, "chebyshev_params_default: null argument");
+    *p = migmres_chebyshev_params{};
+    p->degree = 1;
+    p->max_eigenvalue = std::numeric_limits<double>::quiet_NaN();
+    p->ratio_eigenvalue = 30.0;
+    p->boost_factor = 1.1;
+    p->min_diagonal_value = std::numeric_limits<double>::epsilon();
+    p->eigenvalue_max_iterations = 10;
+    p->zero_starting_solution = 1;
+    p->assume_matrix_unchanged = 0;
+    p->textbook_algorithm = 0;
+    p->seed = 1;
+  });
+}
+
+extern "C" int migmres_chebyshev_create(migmres_crs *A, const migmres_chebyshev_params *p, migmres_prec **out) {
+  return guard([&] {
+    MIG_CHECK(A && p && out, "chebyshev_create: null argument");
+    // Details::Chebyshev::setParameters' checks (:465-582)
+    MIG_CHECK(p->degree >= 0, "\"chebyshev: degree\" must be a nonnegative integer");
+    MIG_CHECK(std::isnan(p->max_eigenvalue) || std::isfinite(p->max_eigenvalue),
+              "\"chebyshev: max eigenvalue\" must be finite");
+    MIG_CHECK(std::isfinite(p->ratio_eigenvalue) && p->ratio_eigenvalue >= 1.0,
+              "\"chebyshev: ratio eigenvalue\" must be finite and >= 1");
+    MIG_CHECK(p->boost_factor >= 1.0, "\"chebyshev: boost factor\" must be >= 1");
+    MIG_CHECK(std::isfinite(p->min_diagonal_value), "\"chebyshev: min diagonal value\" must be finite");
+    MIG_CHECK(p->eigenvalue_max_iterations >= 0, "\"chebyshev: eigenvalue max iterations\" must be nonnegative");
+    std::unique_ptr<migmres_prec> M(new migmres_prec());
+    M->ctx = A->ctx;
+    M->A = A;
+    M->kind = 1;
+    M->cheb = *p;
+    M->cheb_computed_lmax = std::numeric_limits<double>::quiet_NaN();
+    const int n = A->n_local;
+    MIG_HIP(hipMalloc(&M->d_dinv, sizeof(double) * (n > 0 ? n : 1)));
+    launch_diag_recip_threshold(A->ctx->stream, A->d_rowptr, A->d_cols, A->d_vals, n, p->min_diagonal_value,
+                                M->d_dinv);
+    chebyshev_compute(*M);
+    MIG_HIP(hipStreamSynchronize(A->ctx->stream));
+    *out = M.release();
+  });
+}
+
+extern "C" int migmres_chebyshev_lambdas(const migmres_prec *M, double *lmax, double *lmin, double *computed) {
+  return guard([&] {
+    MIG_CHECK(M && M->kind == 1, "chebyshev_lambdas: not a Chebyshev preconditioner");
+    if (lmax) *lmax = M->cheb_lmax;
+    if (lmin) *lmin = M->cheb_lmin;
+    if (computed) *computed = M->cheb_computed_lmax;
   });
 }
 

@@ -187,7 +187,8 @@ struct migmres_crs {
 };
 
 // Point-Jacobi preconditioner (Ifpack2::Relaxation "Jacobi"): Y = M X with `sweeps`
-// sweeps from a zero start, damping `damping` (see prec.cpp).
+// sweeps from a zero start, damping `damping`; or (kind 1) the Chebyshev smoother
+// (Ifpack2::Chebyshev) -- see prec.cpp.
 struct migmres_prec {
   migmres_ctx *ctx = nullptr;
   migmres_crs *A = nullptr;
@@ -199,6 +200,11 @@ struct migmres_prec {
   long long n_apply = 0;
   migmres_mv *work = nullptr;   // residual scratch for sweeps > 1
   migmres_mv *xcopy = nullptr;  // deep copy of X when apply(X, Y) aliases
+  // kind 1: Ifpack2::Chebyshev (prec.cpp); d_dinv holds the reciprocal_threshold diagonal
+  int kind = 0;
+  migmres_chebyshev_params cheb{};
+  double cheb_computed_lmax = 0.0, cheb_lmax = 0.0, cheb_lmin = 0.0, cheb_ratio = 0.0;
+  migmres_mv *cheb_w = nullptr, *cheb_p = nullptr;  // W (and the textbook form's P)
   ~migmres_prec();
 };
 
