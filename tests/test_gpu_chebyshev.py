@@ -52,10 +52,12 @@ def _device_apply(comm, gen, n, B, params, X0=None, seed=1):
     return first, Xd.download(), M.getLambdaMaxForApply(), M.getComputedLambdaMax()
 
 
-def _oracle(gen, n, params, seed=1):
+def _oracle(gen, n, params, seed=1, P=1):
+    """The oracle operator of a P-rank run (the local column order, hence each row's stored
+    order, depends on P: Epetra sorts a row by local index)."""
     from oracle import epetra as oe
     from oracle.ifpack2 import Chebyshev, crs_diagonal_fast
-    A = oe.DistCrs(gen, n, 1)
+    A = oe.DistCrs(gen, n, P)
     rp, gc, vv = gen(0, n)
     return A, Chebyshev(A.apply, crs_diagonal_fast(rp, gc, vv, 0, n), params, seed=seed)
 
@@ -141,7 +143,7 @@ def test_chebyshev_apply_ranks_bit_exact(P):
     n, gen = _laplace2d(30, 29)
     params = {"chebyshev: degree": 5, "chebyshev: max eigenvalue": 1.95}
     B, _ = oe.epetra_random_mv(5, n, 2)
-    _, M = _oracle(gen, n, params)
+    _, M = _oracle(gen, n, params, P=P)
     want = M(B)
     for first, got, _, _ in run_ranks(P, lambda c: _device_apply(c, gen, n, B, params)):
         assert np.array_equal(got, want[first:first + got.shape[0]])
@@ -153,7 +155,7 @@ def test_chebyshev_power_method_estimate(comm, P):
     n, gen = _laplace2d(50, 41)
     params = {"chebyshev: degree": 4, "chebyshev: eigenvalue max iterations": 12}
     B, _ = oe.epetra_random_mv(5, n, 2)
-    _, M = _oracle(gen, n, params, seed=7)
+    _, M = _oracle(gen, n, params, seed=7, P=P)
     want = M(B)
     run = (lambda fn: [fn(comm)]) if P == 1 else (lambda fn: run_ranks(P, fn))
     for first, got, lmax, computed in run(lambda c: _device_apply(c, gen, n, B, params, seed=7)):
