@@ -200,6 +200,10 @@ int migmres_crs_apply(migmres_crs *A, const migmres_mv *X, migmres_mv *Y, double
  * SELL kernel (MIGMRES_NO_BSR3=1 at creation keeps MIGMRES_SPMM_SELL). */
 #define MIGMRES_SPMM_BSR3 5
 int migmres_crs_spmm_kernel(const migmres_crs *A, int *kind);
+/* Digests (64-bit hashes) of the SpMM format plans A holds -- flags, fixed bytes and every
+ * format array -- into out[0 .. n); *needed = the digest count.  Test support: the device
+ * builders (formats.hip) and the host builders (MIGMRES_HOST_FORMATS=1, plan.cpp) must agree. */
+int migmres_crs_format_digest(const migmres_crs *A, unsigned long long *out, int n, int *needed);
 
 /* ---------------- multivectors (Belos::MultiVecTraits) ---------------- */
 

@@ -18,6 +18,8 @@
 // path (tests/test_gpu_fillcomplete.py): same column map, import plan and local CSR.
 #include <hipcub/hipcub.hpp>
 
+#include "formats.h"
+
 #include "plan.h"
 #include "runtime.h"
 
@@ -257,8 +259,10 @@ void fill_complete_device(migmres_crs *A, const long long *d_rowptr, const long 
   if (n_local > 0) k_fc_sort_rows<<<nblk(n_local), 256, 0, s>>>(n_local, d_rowptr, A->d_cols, A->d_vals);
   MIG_HIP(hipGetLastError());
 
-  // the SpMM format plans (pair / template / SELL-64: this library's, not Epetra's) are built
-  // on the host from the finished local CSR
+  // the SpMM format plans (pair / template / SELL-64 / 3x3 blocks: this library's, not
+  // Epetra's) are built on the device from the finished local CSR (formats.hip); only
+  // MIGMRES_HOST_FORMATS=1 brings it to the host for plan.cpp's builders
+  if (!host_formats()) return;
   lcols.resize((size_t)nnz);
   lvals.resize((size_t)nnz);
   if (nnz) {

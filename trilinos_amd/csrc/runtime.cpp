@@ -1,5 +1,6 @@
 // Context, multivectors, distributed CRS operator and the C ABI for them.
 #include "runtime.h"
+#include "formats.h"
 
 #include <chrono>
 #include <algorithm>
@@ -788,6 +789,104 @@ migmres_crs *crs_create_device(migmres_ctx *ctx, long long n_global, long long f
   return A;
 }
 
+static bool env_on(const char *name) {
+  const char *e = std::getenv(name);
+  return e && e[0] == '1';
+}
+
+// The lane-shared form of the templates (k_spmm_tpl3) and the template kernels' knobs.
+static void setup_template_kernels(migmres_crs *A, const PairTemplates &pt) {
+  const char *tsl = std::getenv("MIGMRES_TPL_SLABS");
+  A->tpl_slabs = tsl ? std::atoi(tsl) : 0;
+  const char *tkc = std::getenv("MIGMRES_TPL_KC");
+  A->tpl_kc = tkc ? std::atoi(tkc) : 8;
+  // long templates (27-point stencils): the lane-shared form when the keys come in
+  // x-neighbour triples (k_spmm_tpl3); MIGMRES_NO_TPL3=1 keeps k_spmm_tpl
+  const bool short_ok = env_on("MIGMRES_TPL3_SHORT");  // 7-point templates too (tuning)
+  StencilGroups sg;
+  if (!env_on("MIGMRES_NO_TPL3") && (pt.maxk > 12 || short_ok) && make_stencil_groups(pt, sg) &&
+      (sg.G == 9 || sg.G == 5 || sg.G == 3)) {
+    MIG_HIP(hipMalloc(&A->d_tpl3_grp, sizeof(unsigned long long) * sg.slots.size()));
+    MIG_HIP(hipMemcpy(A->d_tpl3_grp, sg.slots.data(), sizeof(unsigned long long) * sg.slots.size(),
+                      hipMemcpyHostToDevice));
+    A->tpl3_center = sg.center;
+    A->tpl3_G = sg.G;
+    A->use_tpl3 = true;
+    const char *sl = std::getenv("MIGMRES_TPL3_SLABS");
+    A->tpl3_slabs = sl ? std::atoi(sl) : 1;
+    const char *kc = std::getenv("MIGMRES_TPL3_KC");
+    A->tpl3_kc = kc ? std::atoi(kc) : 4;
+  }
+}
+
+// formats.hip: every SpMM format plan and the halo overlap's unit lists from the device CSR.
+static void build_formats_device(migmres_crs *A) {
+  migmres_ctx *ctx = A->ctx;
+  hipStream_t s = ctx->stream;
+  const int n_local = A->n_local;
+  const long long nnz = A->nnz;
+  const DevCsr dc{n_local, nnz, A->d_rowptr, A->d_cols, A->d_vals};
+  if (!env_on("MIGMRES_NO_PAIR_SPMM") && n_local > 0) {
+    DevPairSell ps;
+    if (dev_pair_sell(s, dc, ps)) {
+      A->d_psv = ps.v;
+      A->d_psk = ps.k;
+      A->d_psm = ps.m;
+      A->use_pairs = true;
+      A->pair_max_keys = ps.maxk;
+      A->pair_rmax = ps.rmax;
+    }
+  }
+  if (!A->use_pairs && !env_on("MIGMRES_NO_SELL_SPMM") && n_local > 0) {
+    DevSell64 sp;
+    dev_sell64(s, dc, sp);
+    A->d_soff = sp.off;
+    A->d_slen = sp.len;
+    A->d_scol = sp.cols;
+    A->d_sval = sp.vals;
+    A->use_sell = true;
+    DevBsr3 b3;
+    if (!env_on("MIGMRES_NO_BSR3") && dev_bsr3(s, dc, b3)) {
+      A->d_b3off = b3.off;
+      A->d_b3len = b3.len;
+      A->d_b3col = b3.bcol;
+      A->d_b3val = b3.vals;
+      A->d_b3rest = b3.rest;
+      A->b3_nbr = b3.nbr;
+      A->n_b3rest = b3.n_rest;
+      A->b3_fixed_bytes = 8.0 * 9.0 * (double)b3.nslots + 4.0 * (double)b3.nslots + 4.0 * b3.nbr + b3.rest_bytes;
+      A->use_bsr3 = true;
+    }
+  }
+  A->spmm_fixed_bytes = A->use_bsr3 ? A->b3_fixed_bytes : 12.0 * nnz + 4.0 * (n_local + 1);
+  DevTemplates dt;
+  if (!env_on("MIGMRES_NO_TPL_SPMM") && n_local > 0 && dev_templates(s, dc, dt)) {
+    double rest_bytes = 0.0;
+    A->n_tpl_rest = dev_template_rest(s, dc, dt.id, dt.npairs, A->use_pairs, &A->d_tpl_rest, &rest_bytes);
+    A->d_tpl_id = dt.id;
+    MIG_HIP(hipMalloc(&A->d_tpl_rec, sizeof(int) * dt.rec.size()));
+    MIG_HIP(hipMalloc(&A->d_tpl_val, sizeof(double) * (dt.vals.size() + 1)));
+    MIG_HIP(hipMemcpy(A->d_tpl_rec, dt.rec.data(), sizeof(int) * dt.rec.size(), hipMemcpyHostToDevice));
+    if (!dt.vals.empty())
+      MIG_HIP(hipMemcpy(A->d_tpl_val, dt.vals.data(), sizeof(double) * dt.vals.size(), hipMemcpyHostToDevice));
+    A->tpl_ntpl = dt.ntpl;
+    A->tpl_maxk = dt.maxk;
+    A->tpl_nvals = (int)dt.vals.size();
+    A->use_tpl = true;
+    PairTemplates pt;
+    pt.ntpl = dt.ntpl;
+    pt.maxk = dt.maxk;
+    pt.npairs = dt.npairs;
+    pt.rec = dt.rec;
+    pt.vals = dt.vals;
+    setup_template_kernels(A, pt);
+    A->spmm_fixed_bytes = (double)dt.npairs + 8.0 * dt.rec.size() / 2 + 8.0 * dt.vals.size() + rest_bytes;
+  }
+  if (!A->plan.remote_lids.empty())
+    dev_halo_units(s, dc, A->use_pairs, &A->d_sel_int, &A->n_sel_int, &A->d_sel_bnd, &A->n_sel_bnd);
+  MIG_HIP(hipStreamSynchronize(s));
+}
+
 static void crs_finish(migmres_crs *A, const long long *rowptr, std::vector<int> &lcols, std::vector<double> &lvals) {
   migmres_ctx *ctx = A->ctx;
   const long long first = A->first, nnz = A->nnz;
@@ -863,148 +962,130 @@ static void crs_finish(migmres_crs *A, const long long *rowptr, std::vector<int>
         MIG_HIP(hipMemcpy(A->d_vals, lvals.data(), sizeof(double) * nnz, hipMemcpyHostToDevice));
       }
     }
-    {
-      PairPlan pp;
-      const char *np = std::getenv("MIGMRES_NO_PAIR_SPMM");
-      if (!(np && np[0] == '1') && n_local > 0 && make_pair_plan(n_local, rowptr, lcols.data(), pp)) {
-        PairSell ps;
-        make_pair_sell(n_local, rowptr, lvals.data(), pp, ps);
-        MIG_HIP(hipMalloc(&A->d_psv, sizeof(double) * ps.v.size()));
-        MIG_HIP(hipMalloc(&A->d_psk, sizeof(int) * ps.k.size()));
-        MIG_HIP(hipMalloc(&A->d_psm, sizeof(unsigned short) * ps.m.size()));
-        MIG_HIP(hipMemcpy(A->d_psv, ps.v.data(), sizeof(double) * ps.v.size(), hipMemcpyHostToDevice));
-        MIG_HIP(hipMemcpy(A->d_psk, ps.k.data(), sizeof(int) * ps.k.size(), hipMemcpyHostToDevice));
-        MIG_HIP(hipMemcpy(A->d_psm, ps.m.data(), sizeof(unsigned short) * ps.m.size(), hipMemcpyHostToDevice));
-        A->use_pairs = true;
-        A->pair_max_keys = ps.maxk;
-        A->pair_rmax = ps.rmax;
-      }
-    }
-    {
-      const char *ns = std::getenv("MIGMRES_NO_SELL_SPMM");
-      if (!A->use_pairs && !(ns && ns[0] == '1') && n_local > 0) {
-        Sell64 sp;
-        make_sell64(n_local, rowptr, lcols.data(), lvals.data(), sp);
-        MIG_HIP(hipMalloc(&A->d_soff, sizeof(long long) * sp.off.size()));
-        MIG_HIP(hipMalloc(&A->d_slen, sizeof(int) * sp.len.size()));
-        MIG_HIP(hipMalloc(&A->d_scol, sizeof(int) * (sp.cols.size() + 1)));
-        MIG_HIP(hipMalloc(&A->d_sval, sizeof(double) * (sp.vals.size() + 1)));
-        MIG_HIP(hipMemcpy(A->d_soff, sp.off.data(), sizeof(long long) * sp.off.size(), hipMemcpyHostToDevice));
-        MIG_HIP(hipMemcpy(A->d_slen, sp.len.data(), sizeof(int) * sp.len.size(), hipMemcpyHostToDevice));
-        if (!sp.cols.empty()) {
-          MIG_HIP(hipMemcpy(A->d_scol, sp.cols.data(), sizeof(int) * sp.cols.size(), hipMemcpyHostToDevice));
-          MIG_HIP(hipMemcpy(A->d_sval, sp.vals.data(), sizeof(double) * sp.vals.size(), hipMemcpyHostToDevice));
+    if (host_formats()) {
+      {
+        PairPlan pp;
+        const char *np = std::getenv("MIGMRES_NO_PAIR_SPMM");
+        if (!(np && np[0] == '1') && n_local > 0 && make_pair_plan(n_local, rowptr, lcols.data(), pp)) {
+          PairSell ps;
+          make_pair_sell(n_local, rowptr, lvals.data(), pp, ps);
+          MIG_HIP(hipMalloc(&A->d_psv, sizeof(double) * ps.v.size()));
+          MIG_HIP(hipMalloc(&A->d_psk, sizeof(int) * ps.k.size()));
+          MIG_HIP(hipMalloc(&A->d_psm, sizeof(unsigned short) * ps.m.size()));
+          MIG_HIP(hipMemcpy(A->d_psv, ps.v.data(), sizeof(double) * ps.v.size(), hipMemcpyHostToDevice));
+          MIG_HIP(hipMemcpy(A->d_psk, ps.k.data(), sizeof(int) * ps.k.size(), hipMemcpyHostToDevice));
+          MIG_HIP(hipMemcpy(A->d_psm, ps.m.data(), sizeof(unsigned short) * ps.m.size(), hipMemcpyHostToDevice));
+          A->use_pairs = true;
+          A->pair_max_keys = ps.maxk;
+          A->pair_rmax = ps.rmax;
         }
-        A->use_sell = true;
-        // 3 x 3 block rows detected from the CRS (3-dof meshes): one column id per block and
-        // contiguous operand segments; MIGMRES_NO_BSR3=1 keeps the row kernel for every row
-        const char *nb3 = std::getenv("MIGMRES_NO_BSR3");
-        Bsr3 b3;
-        if (!(nb3 && nb3[0] == '1') && make_bsr3(n_local, rowptr, lcols.data(), lvals.data(), b3)) {
-          MIG_HIP(hipMalloc(&A->d_b3off, sizeof(long long) * b3.off.size()));
-          MIG_HIP(hipMalloc(&A->d_b3len, sizeof(int) * (b3.len.size() + 1)));
-          MIG_HIP(hipMalloc(&A->d_b3col, sizeof(int) * (b3.bcol.size() + 1)));
-          MIG_HIP(hipMalloc(&A->d_b3val, sizeof(double) * (b3.vals.size() + 1)));
-          MIG_HIP(hipMemcpy(A->d_b3off, b3.off.data(), sizeof(long long) * b3.off.size(), hipMemcpyHostToDevice));
-          MIG_HIP(hipMemcpy(A->d_b3len, b3.len.data(), sizeof(int) * b3.len.size(), hipMemcpyHostToDevice));
-          MIG_HIP(hipMemcpy(A->d_b3col, b3.bcol.data(), sizeof(int) * b3.bcol.size(), hipMemcpyHostToDevice));
-          MIG_HIP(hipMemcpy(A->d_b3val, b3.vals.data(), sizeof(double) * b3.vals.size(), hipMemcpyHostToDevice));
-          if (!b3.rest.empty()) {
-            MIG_HIP(hipMalloc(&A->d_b3rest, sizeof(int) * b3.rest.size()));
-            MIG_HIP(hipMemcpy(A->d_b3rest, b3.rest.data(), sizeof(int) * b3.rest.size(), hipMemcpyHostToDevice));
+      }
+      {
+        const char *ns = std::getenv("MIGMRES_NO_SELL_SPMM");
+        if (!A->use_pairs && !(ns && ns[0] == '1') && n_local > 0) {
+          Sell64 sp;
+          make_sell64(n_local, rowptr, lcols.data(), lvals.data(), sp);
+          MIG_HIP(hipMalloc(&A->d_soff, sizeof(long long) * sp.off.size()));
+          MIG_HIP(hipMalloc(&A->d_slen, sizeof(int) * sp.len.size()));
+          MIG_HIP(hipMalloc(&A->d_scol, sizeof(int) * (sp.cols.size() + 1)));
+          MIG_HIP(hipMalloc(&A->d_sval, sizeof(double) * (sp.vals.size() + 1)));
+          MIG_HIP(hipMemcpy(A->d_soff, sp.off.data(), sizeof(long long) * sp.off.size(), hipMemcpyHostToDevice));
+          MIG_HIP(hipMemcpy(A->d_slen, sp.len.data(), sizeof(int) * sp.len.size(), hipMemcpyHostToDevice));
+          if (!sp.cols.empty()) {
+            MIG_HIP(hipMemcpy(A->d_scol, sp.cols.data(), sizeof(int) * sp.cols.size(), hipMemcpyHostToDevice));
+            MIG_HIP(hipMemcpy(A->d_sval, sp.vals.data(), sizeof(double) * sp.vals.size(), hipMemcpyHostToDevice));
           }
-          A->b3_nbr = b3.nbr;
-          A->n_b3rest = (int)b3.rest.size();
-          double rest_bytes = 0.0;
-          for (int r : b3.rest) rest_bytes += 12.0 * (double)(rowptr[r + 1] - rowptr[r]) + 4.0;
-          A->b3_fixed_bytes = 8.0 * b3.vals.size() + 4.0 * b3.bcol.size() + 4.0 * b3.len.size() + rest_bytes;
-          A->use_bsr3 = true;
-        }
-      }
-    }
-    A->spmm_fixed_bytes = A->use_bsr3 ? A->b3_fixed_bytes : 12.0 * nnz + 4.0 * (n_local + 1);
-    {
-      // row-pair templates: the pairs' shapes repeat (stencils) -> one byte per pair
-      const char *nt = std::getenv("MIGMRES_NO_TPL_SPMM");
-      PairTemplates pt;
-      if (!(nt && nt[0] == '1') && n_local > 0 &&
-          make_pair_templates(n_local, rowptr, lcols.data(), lvals.data(), pt)) {
-        std::vector<int> rest;
-        double rest_bytes = 0.0;
-        for (int q = 0; q < pt.npairs; ++q) {
-          if (pt.id[(size_t)q] != kTplNone) continue;
-          if (A->use_pairs) rest.push_back(q);
-          for (int r = 2 * q; r < std::min(n_local, 2 * q + 2); ++r) {
-            if (!A->use_pairs) rest.push_back(r);
-            rest_bytes += 12.0 * (double)(rowptr[r + 1] - rowptr[r]) + 4.0;
-          }
-        }
-        MIG_HIP(hipMalloc(&A->d_tpl_id, pt.id.size()));
-        MIG_HIP(hipMalloc(&A->d_tpl_rec, sizeof(int) * pt.rec.size()));
-        MIG_HIP(hipMalloc(&A->d_tpl_val, sizeof(double) * (pt.vals.size() + 1)));
-        MIG_HIP(hipMemcpy(A->d_tpl_id, pt.id.data(), pt.id.size(), hipMemcpyHostToDevice));
-        MIG_HIP(hipMemcpy(A->d_tpl_rec, pt.rec.data(), sizeof(int) * pt.rec.size(), hipMemcpyHostToDevice));
-        if (!pt.vals.empty())
-          MIG_HIP(hipMemcpy(A->d_tpl_val, pt.vals.data(), sizeof(double) * pt.vals.size(), hipMemcpyHostToDevice));
-        if (!rest.empty()) {
-          MIG_HIP(hipMalloc(&A->d_tpl_rest, sizeof(int) * rest.size()));
-          MIG_HIP(hipMemcpy(A->d_tpl_rest, rest.data(), sizeof(int) * rest.size(), hipMemcpyHostToDevice));
-        }
-        A->n_tpl_rest = (int)rest.size();
-        A->tpl_ntpl = pt.ntpl;
-        A->tpl_maxk = pt.maxk;
-        A->tpl_nvals = (int)pt.vals.size();
-        A->use_tpl = true;
-        const char *tsl = std::getenv("MIGMRES_TPL_SLABS");
-        A->tpl_slabs = tsl ? std::atoi(tsl) : 0;
-        const char *tkc = std::getenv("MIGMRES_TPL_KC");
-        A->tpl_kc = tkc ? std::atoi(tkc) : 8;
-        // long templates (27-point stencils): the lane-shared form when the keys come in
-        // x-neighbour triples (k_spmm_tpl3); MIGMRES_NO_TPL3=1 keeps k_spmm_tpl
-        const char *n3 = std::getenv("MIGMRES_NO_TPL3");
-        const char *s3 = std::getenv("MIGMRES_TPL3_SHORT");  // 7-point templates too (tuning)
-        const bool short_ok = s3 && s3[0] == '1';
-        StencilGroups sg;
-        if (!(n3 && n3[0] == '1') && (pt.maxk > 12 || short_ok) && make_stencil_groups(pt, sg) &&
-            (sg.G == 9 || sg.G == 5 || sg.G == 3)) {
-          MIG_HIP(hipMalloc(&A->d_tpl3_grp, sizeof(unsigned long long) * sg.slots.size()));
-          MIG_HIP(hipMemcpy(A->d_tpl3_grp, sg.slots.data(), sizeof(unsigned long long) * sg.slots.size(),
-                            hipMemcpyHostToDevice));
-          A->tpl3_center = sg.center;
-          A->tpl3_G = sg.G;
-          A->use_tpl3 = true;
-          const char *sl = std::getenv("MIGMRES_TPL3_SLABS");
-          A->tpl3_slabs = sl ? std::atoi(sl) : 1;
-          const char *kc = std::getenv("MIGMRES_TPL3_KC");
-          A->tpl3_kc = kc ? std::atoi(kc) : 4;
-        }
-        A->spmm_fixed_bytes = (double)pt.npairs + 8.0 * pt.rec.size() / 2 + 8.0 * pt.vals.size() + rest_bytes;
-      }
-    }
-    if (n_remote > 0) {
-      // interior / boundary units for the halo overlap (a unit is a row pair with the
-      // row-pair kernel, else a row; boundary = reads at least one ghost column)
-      const int unit = A->use_pairs ? 2 : 1;
-      const int nunits = (n_local + unit - 1) / unit;
-      std::vector<int> sel_int, sel_bnd;
-      for (int u = 0; u < nunits; ++u) {
-        bool ghost = false;
-        for (int r = u * unit; r < std::min(n_local, (u + 1) * unit) && !ghost; ++r)
-          for (long long e = rowptr[r]; e < rowptr[r + 1]; ++e)
-            if (lcols[(size_t)e] >= n_local) {
-              ghost = true;
-              break;
+          A->use_sell = true;
+          // 3 x 3 block rows detected from the CRS (3-dof meshes): one column id per block and
+          // contiguous operand segments; MIGMRES_NO_BSR3=1 keeps the row kernel for every row
+          const char *nb3 = std::getenv("MIGMRES_NO_BSR3");
+          Bsr3 b3;
+          if (!(nb3 && nb3[0] == '1') && make_bsr3(n_local, rowptr, lcols.data(), lvals.data(), b3)) {
+            MIG_HIP(hipMalloc(&A->d_b3off, sizeof(long long) * b3.off.size()));
+            MIG_HIP(hipMalloc(&A->d_b3len, sizeof(int) * (b3.len.size() + 1)));
+            MIG_HIP(hipMalloc(&A->d_b3col, sizeof(int) * (b3.bcol.size() + 1)));
+            MIG_HIP(hipMalloc(&A->d_b3val, sizeof(double) * (b3.vals.size() + 1)));
+            MIG_HIP(hipMemcpy(A->d_b3off, b3.off.data(), sizeof(long long) * b3.off.size(), hipMemcpyHostToDevice));
+            MIG_HIP(hipMemcpy(A->d_b3len, b3.len.data(), sizeof(int) * b3.len.size(), hipMemcpyHostToDevice));
+            MIG_HIP(hipMemcpy(A->d_b3col, b3.bcol.data(), sizeof(int) * b3.bcol.size(), hipMemcpyHostToDevice));
+            MIG_HIP(hipMemcpy(A->d_b3val, b3.vals.data(), sizeof(double) * b3.vals.size(), hipMemcpyHostToDevice));
+            if (!b3.rest.empty()) {
+              MIG_HIP(hipMalloc(&A->d_b3rest, sizeof(int) * b3.rest.size()));
+              MIG_HIP(hipMemcpy(A->d_b3rest, b3.rest.data(), sizeof(int) * b3.rest.size(), hipMemcpyHostToDevice));
             }
-        (ghost ? sel_bnd : sel_int).push_back(u);
+            A->b3_nbr = b3.nbr;
+            A->n_b3rest = (int)b3.rest.size();
+            double rest_bytes = 0.0;
+            for (int r : b3.rest) rest_bytes += 12.0 * (double)(rowptr[r + 1] - rowptr[r]) + 4.0;
+            A->b3_fixed_bytes = 8.0 * b3.vals.size() + 4.0 * b3.bcol.size() + 4.0 * b3.len.size() + rest_bytes;
+            A->use_bsr3 = true;
+          }
+        }
       }
-      A->n_sel_int = (int)sel_int.size();
-      A->n_sel_bnd = (int)sel_bnd.size();
-      MIG_HIP(hipMalloc(&A->d_sel_int, sizeof(int) * (sel_int.size() + 1)));
-      MIG_HIP(hipMalloc(&A->d_sel_bnd, sizeof(int) * (sel_bnd.size() + 1)));
-      if (!sel_int.empty())
-        MIG_HIP(hipMemcpy(A->d_sel_int, sel_int.data(), sizeof(int) * sel_int.size(), hipMemcpyHostToDevice));
-      if (!sel_bnd.empty())
-        MIG_HIP(hipMemcpy(A->d_sel_bnd, sel_bnd.data(), sizeof(int) * sel_bnd.size(), hipMemcpyHostToDevice));
+      A->spmm_fixed_bytes = A->use_bsr3 ? A->b3_fixed_bytes : 12.0 * nnz + 4.0 * (n_local + 1);
+      {
+        // row-pair templates: the pairs' shapes repeat (stencils) -> one byte per pair
+        const char *nt = std::getenv("MIGMRES_NO_TPL_SPMM");
+        PairTemplates pt;
+        if (!(nt && nt[0] == '1') && n_local > 0 &&
+            make_pair_templates(n_local, rowptr, lcols.data(), lvals.data(), pt)) {
+          std::vector<int> rest;
+          double rest_bytes = 0.0;
+          for (int q = 0; q < pt.npairs; ++q) {
+            if (pt.id[(size_t)q] != kTplNone) continue;
+            if (A->use_pairs) rest.push_back(q);
+            for (int r = 2 * q; r < std::min(n_local, 2 * q + 2); ++r) {
+              if (!A->use_pairs) rest.push_back(r);
+              rest_bytes += 12.0 * (double)(rowptr[r + 1] - rowptr[r]) + 4.0;
+            }
+          }
+          MIG_HIP(hipMalloc(&A->d_tpl_id, pt.id.size()));
+          MIG_HIP(hipMalloc(&A->d_tpl_rec, sizeof(int) * pt.rec.size()));
+          MIG_HIP(hipMalloc(&A->d_tpl_val, sizeof(double) * (pt.vals.size() + 1)));
+          MIG_HIP(hipMemcpy(A->d_tpl_id, pt.id.data(), pt.id.size(), hipMemcpyHostToDevice));
+          MIG_HIP(hipMemcpy(A->d_tpl_rec, pt.rec.data(), sizeof(int) * pt.rec.size(), hipMemcpyHostToDevice));
+          if (!pt.vals.empty())
+            MIG_HIP(hipMemcpy(A->d_tpl_val, pt.vals.data(), sizeof(double) * pt.vals.size(), hipMemcpyHostToDevice));
+          if (!rest.empty()) {
+            MIG_HIP(hipMalloc(&A->d_tpl_rest, sizeof(int) * rest.size()));
+            MIG_HIP(hipMemcpy(A->d_tpl_rest, rest.data(), sizeof(int) * rest.size(), hipMemcpyHostToDevice));
+          }
+          A->n_tpl_rest = (int)rest.size();
+          A->tpl_ntpl = pt.ntpl;
+          A->tpl_maxk = pt.maxk;
+          A->tpl_nvals = (int)pt.vals.size();
+          A->use_tpl = true;
+          setup_template_kernels(A, pt);
+          A->spmm_fixed_bytes = (double)pt.npairs + 8.0 * pt.rec.size() / 2 + 8.0 * pt.vals.size() + rest_bytes;
+        }
+      }
+      if (n_remote > 0) {
+        // interior / boundary units for the halo overlap (a unit is a row pair with the
+        // row-pair kernel, else a row; boundary = reads at least one ghost column)
+        const int unit = A->use_pairs ? 2 : 1;
+        const int nunits = (n_local + unit - 1) / unit;
+        std::vector<int> sel_int, sel_bnd;
+        for (int u = 0; u < nunits; ++u) {
+          bool ghost = false;
+          for (int r = u * unit; r < std::min(n_local, (u + 1) * unit) && !ghost; ++r)
+            for (long long e = rowptr[r]; e < rowptr[r + 1]; ++e)
+              if (lcols[(size_t)e] >= n_local) {
+                ghost = true;
+                break;
+              }
+          (ghost ? sel_bnd : sel_int).push_back(u);
+        }
+        A->n_sel_int = (int)sel_int.size();
+        A->n_sel_bnd = (int)sel_bnd.size();
+        MIG_HIP(hipMalloc(&A->d_sel_int, sizeof(int) * (sel_int.size() + 1)));
+        MIG_HIP(hipMalloc(&A->d_sel_bnd, sizeof(int) * (sel_bnd.size() + 1)));
+        if (!sel_int.empty())
+          MIG_HIP(hipMemcpy(A->d_sel_int, sel_int.data(), sizeof(int) * sel_int.size(), hipMemcpyHostToDevice));
+        if (!sel_bnd.empty())
+          MIG_HIP(hipMemcpy(A->d_sel_bnd, sel_bnd.data(), sizeof(int) * sel_bnd.size(), hipMemcpyHostToDevice));
+      }
+    } else {
+      build_formats_device(A);
     }
     auto upload_groups = [](const std::vector<migmres_crs::Nbr> &nbrs, size_t n, int2 **out) {
       std::vector<int2> g(n);
@@ -1190,6 +1271,75 @@ extern "C" int migmres_crs_spmm_kernel(const migmres_crs *A, int *kind) {
             : A->use_pairs ? MIGMRES_SPMM_PAIR
             : A->use_sell  ? MIGMRES_SPMM_SELL
                            : MIGMRES_SPMM_CSR;
+  });
+}
+namespace {
+unsigned long long fnv_bytes(const void *d_ptr, size_t bytes) {
+  unsigned long long h = 0xcbf29ce484222325ULL;
+  if (!d_ptr || bytes == 0) return h;
+  std::vector<unsigned char> buf(bytes);
+  MIG_HIP(hipMemcpy(buf.data(), d_ptr, bytes, hipMemcpyDeviceToHost));
+  for (unsigned char b : buf) h = (h ^ b) * 0x100000001b3ULL;
+  return h;
+}
+}  // namespace
+
+extern "C" int migmres_crs_format_digest(const migmres_crs *A, unsigned long long *out, int n, int *needed) {
+  return guard([&] {
+    MIG_CHECK(A, "bad arguments");
+    MIG_HIP(hipStreamSynchronize(A->ctx->stream));
+    std::vector<unsigned long long> d;
+    auto num = [&](double v) {
+      unsigned long long b;
+      std::memcpy(&b, &v, sizeof(b));
+      d.push_back(b);
+    };
+    const int nl = A->n_local, P = (nl + 1) / 2;
+    d.push_back((unsigned long long)A->use_pairs | (unsigned long long)A->use_sell << 1 |
+                (unsigned long long)A->use_bsr3 << 2 | (unsigned long long)A->use_tpl << 3 |
+                (unsigned long long)A->use_tpl3 << 4);
+    num(A->spmm_fixed_bytes);
+    if (A->use_pairs) {
+      const size_t nch = (size_t)(P + 63) / 64;
+      d.push_back((unsigned long long)A->pair_max_keys << 32 | (unsigned)A->pair_rmax);
+      d.push_back(fnv_bytes(A->d_psv, sizeof(double) * nch * 2 * A->pair_rmax * 64));
+      d.push_back(fnv_bytes(A->d_psk, sizeof(int) * nch * A->pair_max_keys * 64));
+      d.push_back(fnv_bytes(A->d_psm, sizeof(unsigned short) * nch * A->pair_max_keys * 64));
+    }
+    if (A->use_sell) {
+      const size_t nch = (size_t)(nl + 63) / 64;
+      long long total = 0;
+      MIG_HIP(hipMemcpy(&total, A->d_soff + nch, sizeof(long long), hipMemcpyDeviceToHost));
+      d.push_back(fnv_bytes(A->d_soff, sizeof(long long) * (nch + 1)));
+      d.push_back(fnv_bytes(A->d_slen, sizeof(int) * nl));
+      d.push_back(fnv_bytes(A->d_scol, sizeof(int) * total));
+      d.push_back(fnv_bytes(A->d_sval, sizeof(double) * total));
+    }
+    if (A->use_bsr3) {
+      const size_t nch = (size_t)(A->b3_nbr + 63) / 64;
+      long long slots = 0;
+      MIG_HIP(hipMemcpy(&slots, A->d_b3off + nch, sizeof(long long), hipMemcpyDeviceToHost));
+      num(A->b3_fixed_bytes);
+      d.push_back(fnv_bytes(A->d_b3off, sizeof(long long) * (nch + 1)));
+      d.push_back(fnv_bytes(A->d_b3len, sizeof(int) * A->b3_nbr));
+      d.push_back(fnv_bytes(A->d_b3col, sizeof(int) * slots));
+      d.push_back(fnv_bytes(A->d_b3val, sizeof(double) * 9 * slots));
+      d.push_back(fnv_bytes(A->d_b3rest, sizeof(int) * A->n_b3rest));
+    }
+    if (A->use_tpl) {
+      d.push_back((unsigned long long)A->tpl_ntpl << 40 | (unsigned long long)A->tpl_maxk << 20 |
+                  (unsigned)A->tpl_nvals);
+      d.push_back(fnv_bytes(A->d_tpl_id, (size_t)P));
+      d.push_back(fnv_bytes(A->d_tpl_rec, sizeof(int) * 2 * (size_t)A->tpl_ntpl * A->tpl_maxk));
+      d.push_back(fnv_bytes(A->d_tpl_val, sizeof(double) * A->tpl_nvals));
+      d.push_back(fnv_bytes(A->d_tpl_rest, sizeof(int) * A->n_tpl_rest));
+    }
+    if (A->use_tpl3) d.push_back(fnv_bytes(A->d_tpl3_grp, sizeof(unsigned long long) * A->tpl_ntpl * A->tpl3_G));
+    d.push_back((unsigned long long)A->n_sel_int << 32 | (unsigned)A->n_sel_bnd);
+    d.push_back(fnv_bytes(A->d_sel_int, sizeof(int) * A->n_sel_int));
+    d.push_back(fnv_bytes(A->d_sel_bnd, sizeof(int) * A->n_sel_bnd));
+    if (needed) *needed = (int)d.size();
+    for (int i = 0; i < n && i < (int)d.size(); ++i) out[i] = d[(size_t)i];
   });
 }
 extern "C" int migmres_map_uniform(long long n_global, int nranks, int rank, long long *first,

@@ -176,11 +176,20 @@ class CrsMatrix:
         return cls(comm, ng.value, _handle=h)
 
     def spmm_kernel(self):
-        """The SpMM kernel apply() runs: "csr", "pair", "sell", "tpl" or "tpl3"
+        """The SpMM kernel apply() runs: "csr", "pair", "sell", "tpl", "tpl3" or "bsr3"
         (migmres_crs_spmm_kernel)."""
         v = C.c_int()
         call("migmres_crs_spmm_kernel", self.h, C.byref(v))
         return ("csr", "pair", "sell", "tpl", "tpl3", "bsr3")[v.value]
+
+    def format_digest(self):
+        """64-bit digests of the SpMM format plans this operator holds
+        (migmres_crs_format_digest): equal lists = identical plans."""
+        need = C.c_int()
+        call("migmres_crs_format_digest", self.h, None, 0, C.byref(need))
+        out = (C.c_ulonglong * max(need.value, 1))()
+        call("migmres_crs_format_digest", self.h, out, need.value, C.byref(need))
+        return list(out)[:need.value]
 
     def colmap(self):
         out = np.empty(self.n_cols, dtype=np.int64)
