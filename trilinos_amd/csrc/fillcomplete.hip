@@ -175,6 +175,7 @@ void fill_complete_device(migmres_crs *A, const long long *d_rowptr, const long 
   if (nnz) MIG_HIP(hipMemcpyAsync(A->d_vals, d_vals_in, sizeof(double) * nnz, hipMemcpyDeviceToDevice, s));
   k_fc_rowptr32<<<nblk(n_local + 1), 256, 0, s>>>(d_rowptr, A->d_rowptr, n_local + 1);
 
+  setup_mark("fc: rowptr + alloc");
   // 1. classify entries, mark present owned columns, collect remote (id, entry) pairs
   DevBuf present((size_t)n_local), counter(sizeof(int)), bad(sizeof(int));
   DevBuf rem_g(sizeof(long long) * (size_t)nnz), rem_e(sizeof(int) * (size_t)nnz);
@@ -209,6 +210,7 @@ void fill_complete_device(migmres_crs *A, const long long *d_rowptr, const long 
     MIG_HIP(hipStreamSynchronize(s));
   }
 
+  setup_mark("fc: classify + remotes");
   // 3. MakeColMap's remote order (Epetra_Util::Sort by owner PID, host: n_remote ids) and the
   //    column map: the owned columns that occur (all of them when every one occurs), then
   //    the remotes
@@ -242,6 +244,7 @@ void fill_complete_device(migmres_crs *A, const long long *d_rowptr, const long 
   const int n_remote = (int)A->plan.remote_gids.size();
   MIG_CHECK(n_remote == (int)remote.size(), "device FillComplete: remote lists disagree");
 
+  setup_mark("fc: colmap + import");
   // 4. remote X-space ids (ghost slot = import order), 5. SortEntries
   if (n_remote > 0) {
     DevBuf rg(sizeof(long long) * n_remote), slot(sizeof(int) * n_remote), sg(sizeof(long long) * n_remote),

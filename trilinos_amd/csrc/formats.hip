@@ -6,6 +6,8 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
@@ -497,6 +499,21 @@ __global__ void k_unit_ghost(const int *rowptr, const int *cols, int n, int nuni
 
 }  // namespace
 
+void setup_mark(const char *what) {
+  static const bool on = [] {
+    const char *e = std::getenv("MIGMRES_SETUP_TRACE");
+    return e && e[0] == '1';
+  }();
+  if (!on) return;
+  static auto t0 = std::chrono::steady_clock::now();
+  static auto last = t0;
+  const auto now = std::chrono::steady_clock::now();
+  std::fprintf(stderr, "[setup] %-28s +%8.1f ms (%8.1f ms)\n", what,
+               std::chrono::duration<double, std::milli>(now - last).count(),
+               std::chrono::duration<double, std::milli>(now - t0).count());
+  last = now;
+}
+
 bool host_formats() {
   const char *e = std::getenv("MIGMRES_HOST_FORMATS");
   return e && e[0] == '1';
@@ -506,6 +523,7 @@ bool dev_pair_sell(hipStream_t s, const DevCsr &A, DevPairSell &out) {
   const int n = A.n_local, P = (n + 1) / 2;
   if (P <= 0) return false;
   Buf nk(sizeof(int) * P), rlen(sizeof(int) * P);
+  setup_mark("formats: pair plan");
   k_pp_count<<<nblk(P), 256, 0, s>>>(A.rowptr, A.cols, n, P, nk.as<int>(), rlen.as<int>());
   MIG_HIP(hipGetLastError());
   if (dev_min<int>(s, nk.as<int>(), P, 0) < 0) return false;  // a pair the plan cannot take
@@ -586,6 +604,7 @@ bool dev_templates(hipStream_t s, const DevCsr &A, DevTemplates &out) {
   out.npairs = P;
   if (P <= 0) return false;
   Buf bad((size_t)P), ghost((size_t)P), cnt(sizeof(long long) * P), eoff(sizeof(long long) * (P + 1));
+  setup_mark("formats: templates");
   k_tpl_check<<<nblk(P), 256, 0, s>>>(A.rowptr, A.cols, n, P, bad.as<unsigned char>(), ghost.as<unsigned char>(),
                                        cnt.as<long long>());
   MIG_HIP(hipGetLastError());

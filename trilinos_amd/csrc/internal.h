@@ -164,4 +164,7 @@ void launch_pack(hipStream_t s, MvDesc X, const int *lids, const int2 *grp, int 
 void launch_unpack(hipStream_t s, const double *recv, const int2 *grp, int count, int k, double *ghost,
                    long long ldg);
 
+// MIGMRES_SETUP_TRACE=1: wall-clock checkpoints of operator setup on stderr (tuning aid).
+void setup_mark(const char *what);
+
 }  // namespace migmres

@@ -779,9 +779,12 @@ migmres_crs *crs_create_device(migmres_ctx *ctx, long long n_global, long long f
     std::vector<long long> rowptr;
     std::vector<int> lcols;
     std::vector<double> lvals;
+    setup_mark("crs_create_device");
     fill_complete_device(A, d_rowptr, d_gcols, d_vals, rowptr, lcols, lvals);
+    setup_mark("fill_complete_device");
     if (!A->nnz && (int)rowptr.size() > n_local) A->nnz = rowptr[(size_t)n_local];
     crs_finish(A, rowptr.data(), lcols, lvals);
+    setup_mark("crs_finish");
   } catch (...) {
     delete A;
     throw;
@@ -1085,7 +1088,9 @@ static void crs_finish(migmres_crs *A, const long long *rowptr, std::vector<int>
           MIG_HIP(hipMemcpy(A->d_sel_bnd, sel_bnd.data(), sizeof(int) * sel_bnd.size(), hipMemcpyHostToDevice));
       }
     } else {
+      setup_mark("crs_finish: before formats");
       build_formats_device(A);
+      setup_mark("crs_finish: formats");
     }
     auto upload_groups = [](const std::vector<migmres_crs::Nbr> &nbrs, size_t n, int2 **out) {
       std::vector<int2> g(n);
