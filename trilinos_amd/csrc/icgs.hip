@@ -327,6 +327,9 @@ void launch_gemm_nn_dot(hipStream_t s, MvDesc A, int L, const double *M, int ldm
 // LDS: Qs[Lp][17] (odd stride: both phases' reads are conflict-free), Xs[16][16], red[4][4][64].
 // -------------------------------------------------------------------------------------
 constexpr int NT_ROWS = 16, NT_MAXL = 256, NT_LDQ = 17;
+#ifndef NT_GS
+#define NT_GS 0
+#endif
 #ifndef NT_DIAG_MASK  // bit 0 phase 1, bit 1 phase 2, bit 2 LDS staging, bit 3 X1 traffic (tools/mb_nntn.hip)
 #define NT_DIAG_MASK 15
 #endif
@@ -685,7 +688,10 @@ __global__ __launch_bounds__(NT) void k_nn_tn_w(MvDesc Q, int L, const double *_
   const int xo = 16 * (xr16 & 3) + 4 * (xr16 >> 2) + (xj & 3);  // D lane of (row, column)
   double *xs = Qs + (size_t)(L + xj) * LDQ + xr;
   const long long nchunks = (nrows + RW - 1) / RW;
-  const long long c0 = nchunks * rng / nrng, c1 = nchunks * (rng + 1) / nrng;
+  // chunk order: workgroup rng owns [c0, c1) (NT_GS = 0), or takes every nrng-th chunk from
+  // rng on (NT_GS = 1: the resident grid sweeps one contiguous band of rows at a time)
+  const long long c0 = NT_GS ? rng : nchunks * rng / nrng, c1 = NT_GS ? nchunks : nchunks * (rng + 1) / nrng;
+  const long long cstep = NT_GS ? nrng : 1;
 
   // (A 2-deep prefetch measured no faster: for the 32-row, C1-in-LDS form at one workgroup
   // per CU, where the LDS reads -- about 200 ds_read_b64 per wave per chunk -- bound it, and
@@ -773,7 +779,7 @@ __global__ __launch_bounds__(NT) void k_nn_tn_w(MvDesc Q, int L, const double *_
 #pragma unroll
     for (int m = 0; m < NLD; ++m) p[m] = *(const d2 *)(lsrc[m] + cf * RW);
     if ((NT_DIAG_MASK & 8) && ST) pout[0] = 0.0;
-    for (long long ch = c0; ch < c1; ++ch) body(p, ch, ch + 1);
+    for (long long ch = c0; ch < c1; ch += cstep) body(p, ch, ch + cstep);
   }
   // partial (L x k) of this workgroup: tile tt rows 16 tt + 4 b + m
   double *out = pout;
