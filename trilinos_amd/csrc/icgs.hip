@@ -603,12 +603,16 @@ static size_t nw_lds_bytes(int L, int NJ, int LX = 0) {
   return sizeof(double) * ((size_t)Lp * (RW + 1) + (NT / 64) * NJ * 64 + (size_t)Lq * 4 * NJ);
 }
 
-template <int RW, int NM, int NJ, bool ST, int NT = 16 * RW>
+template <int RW, int NM, int NJ, bool ST, int NT = 16 * RW, int VIS = RW>
 __global__ __launch_bounds__(NT) void k_nn_tn_w(MvDesc Q, int L, const double *__restrict__ C1, int ldc,
                                                 MvDesc X, int kx, int nrows, double *__restrict__ partial,
                                                 double *__restrict__ sink) {
   // NT threads: 16 RW (phase 1 in K quarters) or, for RW = 16, 512 (K eighths: KQ = 8)
-  constexpr int NTH = NT, NWAVE = NTH / 64, RB = RW / 16, KQ = NWAVE / RB, LDQ = RW + 1, LPC = RW / 2;
+  // VIS rows per column visit: RW (each chunk loaded on its own), or 2 RW for RW = 16 (a
+  // 32-row visit -- 256 B per column -- loaded at once and published to the 16-row image in
+  // two halves; the 16-row form's 128-byte visits stream at ~4-4.6 TB/s, 256-byte ones ~5.6)
+  static_assert(VIS == RW || (RW == 16 && VIS == 32 && NT == 256 && !ST), "visit = chunk, or 2 x 16 rows read-only");
+  constexpr int NTH = NT, NWAVE = NTH / 64, RB = RW / 16, KQ = NWAVE / RB, LDQ = RW + 1, LPC = VIS / 2;
   constexpr int CPR = NTH / LPC, NLD = (32 * NM + CPR - 1) / CPR, MS = (8 * NM + KQ - 1) / KQ;
   extern __shared__ __attribute__((aligned(16))) double sm[];
   // kx > 8: workgroup pairs take the two column halves of X (columns h0 .. h0 + k - 1) over
@@ -639,7 +643,7 @@ __global__ __launch_bounds__(NT) void k_nn_tn_w(MvDesc Q, int L, const double *_
   // steps kq, kq + 4, ...), so each lane keeps its C1 entries in registers -- 4 of the 5 LDS
   // reads per phase-1 MFMA step at k = 16.  Wider images would need more than the 256
   // registers per lane that two waves per SIMD leave (2 NM x 4 doubles of C1 alone).
-  constexpr bool CREG = nw_creg<RW, NT>(NM);
+  constexpr bool CREG = nw_creg<RW, NT>(NM) && VIS == RW;
   double c1r[CREG ? MS : 1][NJ];
   if constexpr (CREG) {
 #pragma unroll
@@ -668,13 +672,14 @@ __global__ __launch_bounds__(NT) void k_nn_tn_w(MvDesc Q, int L, const double *_
   // loader: staged column lcol + 32 m (clamped to LX - 1: duplicates rewrite the same
   // value), rows lrow, lrow + 1 of the chunk; staged columns >= L come from X.
   const int lrow = 2 * (t % LPC), lcol = t / LPC;
+  const int lhalf = lrow / RW;  // VIS = 2 RW: the half of the visit this lane's rows are in
   const double *lsrc[NLD];
   int lsts[NLD];
 #pragma unroll
   for (int m = 0; m < NLD; ++m) {
     int i = lcol + CPR * m;
     i = i < LX ? i : LX - 1;
-    lsts[m] = i * LDQ + lrow;
+    lsts[m] = i * LDQ + lrow % RW;
     lsrc[m] = (i < L ? colp_(Q, i) : xcol(i - L)) + lrow;
   }
   // X1 element e = t mod (RW k): row xr of column xj.  Threads t >= RW k repeat an element
@@ -702,74 +707,111 @@ __global__ __launch_bounds__(NT) void k_nn_tn_w(MvDesc Q, int L, const double *_
   // vmcnt(1) for the last prefetched column instead of vmcnt(0) (which waits for the X1
   // store's completion).  partial[0] of this workgroup is rewritten at the end.
   // One chunk: publish the prefetched image pp, refill pp with chunk `nxt`, both phases.
-  auto body = [&](d2(&pp)[NLD], long long ch, long long nxt) {
-    const long long r0 = ch * RW;
+  // publish the prefetched visit (VIS = 2 RW: only the lanes holding half h write)
+  auto publish = [&](d2(&pp)[NLD], int h) __attribute__((always_inline)) {
+    const bool mine = VIS == RW || lhalf == h;
 #pragma unroll
     for (int m = 0; m < NLD; ++m) {
       if (NT_DIAG_MASK & 4) {
-        Qs[lsts[m]] = pp[m].x;
-        Qs[lsts[m] + 1] = pp[m].y;
+        if (mine) {
+          Qs[lsts[m]] = pp[m].x;
+          Qs[lsts[m] + 1] = pp[m].y;
+        }
       } else if (pp[m].x == 12345.0) {
         Qs[0] = pp[m].y;
       }
     }
+  };
+  // both phases on chunk ch of the published image
+  auto compute = [&](long long ch) __attribute__((always_inline)) {
+    const long long r0 = ch * RW;
+    const double xval = *xs;
+    // phase 1: rows 16 rb .. 16 rb + 15, K steps s = kq + KQ m (4 s < L <= 32 NM)
+    double a1[NJ];
+#pragma unroll
+    for (int jg = 0; jg < NJ; ++jg) a1[jg] = 0.0;
+#pragma unroll
+    for (int m = 0; m < ((NT_DIAG_MASK & 1) ? MS : 0); ++m) {
+      const int s = kq + KQ * m;
+      if (4 * s < L) {
+        const double qa = Qs[(4 * s + g) * LDQ + 16 * rb + c];
+#pragma unroll
+        for (int jg = 0; jg < NJ; ++jg)
+          a1[jg] = mfma4(qa, CREG ? c1r[CREG ? m : 0][jg] : C1s[(4 * s + g) * 4 * NJ + 4 * jg + n4], a1[jg]);
+      }
+    }
+#pragma unroll
+    for (int jg = 0; jg < NJ; ++jg) red[((kq * RB + rb) * NJ + jg) * 64 + l] = a1[jg];
+    lds_barrier();
+    {
+      auto rd = [&](int q) { return red[((q * RB + xrb) * NJ + xjg) * 64 + xo]; };
+      double d = (rd(0) + rd(1)) + (rd(2) + rd(3));
+      if constexpr (KQ == 8) d += (rd(4) + rd(5)) + (rd(6) + rd(7));
+      const double x1 = xval - d;
+      if ((NT_DIAG_MASK & 8) && ST) xdst[r0 + xr] = x1;
+      if (xprim) *xs = x1;
+    }
+    lds_barrier();
+    // phase 2: tiles w, w + NWAVE, ... against the RW rows of X1 (staged columns L + j); a
+    // K step's X1 operands are read once and reused by all of the wave's tiles (LDS reads
+    // per wave and chunk: RW/4 (NJ + TPW) instead of RW/4 TPW (1 + NJ))
+    if (NT_DIAG_MASK & 2) {
+#pragma unroll
+      for (int s = 0; s < RW / 4; ++s) {
+        double xb[NJ];
+#pragma unroll
+        for (int jg = 0; jg < NJ; ++jg) xb[jg] = Qs[(L + 4 * jg + n4) * LDQ + 4 * s + g];
+#pragma unroll
+        for (int mm = 0; mm < TPW; ++mm) {
+          const int tt = w + NWAVE * mm;
+          if (16 * tt < L) {
+            const double qa = Qs[(16 * tt + c) * LDQ + 4 * s + g];
+#pragma unroll
+            for (int jg = 0; jg < NJ; ++jg) acc2[mm][jg] = mfma4(qa, xb[jg], acc2[mm][jg]);
+          }
+        }
+      }
+    }
+  };
+  auto body = [&](d2(&pp)[NLD], long long ch, long long nxt) {
+    publish(pp, 0);
     lds_barrier();
     {
       const long long cn = clampc(nxt) * RW;
 #pragma unroll
       for (int m = 0; m < NLD; ++m) pp[m] = *(const d2 *)(lsrc[m] + cn);
     }
-    if (ch < c1) {
-      const double xval = *xs;
-      // phase 1: rows 16 rb .. 16 rb + 15, K steps s = kq + KQ m (4 s < L <= 32 NM)
-      double a1[NJ];
-#pragma unroll
-      for (int jg = 0; jg < NJ; ++jg) a1[jg] = 0.0;
-#pragma unroll
-      for (int m = 0; m < ((NT_DIAG_MASK & 1) ? MS : 0); ++m) {
-        const int s = kq + KQ * m;
-        if (4 * s < L) {
-          const double qa = Qs[(4 * s + g) * LDQ + 16 * rb + c];
-#pragma unroll
-          for (int jg = 0; jg < NJ; ++jg)
-            a1[jg] = mfma4(qa, CREG ? c1r[CREG ? m : 0][jg] : C1s[(4 * s + g) * 4 * NJ + 4 * jg + n4], a1[jg]);
-        }
-      }
-#pragma unroll
-      for (int jg = 0; jg < NJ; ++jg) red[((kq * RB + rb) * NJ + jg) * 64 + l] = a1[jg];
-      lds_barrier();
-      {
-        auto rd = [&](int q) { return red[((q * RB + xrb) * NJ + xjg) * 64 + xo]; };
-        double d = (rd(0) + rd(1)) + (rd(2) + rd(3));
-        if constexpr (KQ == 8) d += (rd(4) + rd(5)) + (rd(6) + rd(7));
-        const double x1 = xval - d;
-        if ((NT_DIAG_MASK & 8) && ST) xdst[r0 + xr] = x1;
-        if (xprim) *xs = x1;
-      }
-      lds_barrier();
-      // phase 2: tiles w, w + NWAVE, ... against the RW rows of X1 (staged columns L + j); a
-      // K step's X1 operands are read once and reused by all of the wave's tiles (LDS reads
-      // per wave and chunk: RW/4 (NJ + TPW) instead of RW/4 TPW (1 + NJ))
-      if (NT_DIAG_MASK & 2) {
-#pragma unroll
-        for (int s = 0; s < RW / 4; ++s) {
-          double xb[NJ];
-#pragma unroll
-          for (int jg = 0; jg < NJ; ++jg) xb[jg] = Qs[(L + 4 * jg + n4) * LDQ + 4 * s + g];
-#pragma unroll
-          for (int mm = 0; mm < TPW; ++mm) {
-            const int tt = w + NWAVE * mm;
-            if (16 * tt < L) {
-              const double qa = Qs[(16 * tt + c) * LDQ + 4 * s + g];
-#pragma unroll
-              for (int jg = 0; jg < NJ; ++jg) acc2[mm][jg] = mfma4(qa, xb[jg], acc2[mm][jg]);
-            }
-          }
-        }
-      }
-    }
+    if (ch < c1) compute(ch);
     lds_barrier();
   };
+  if constexpr (VIS != RW) {
+    // 32-row visits (RW = 16): visit v = chunks 2v, 2v + 1, loaded by one set of 16-byte loads
+    // (16 lanes per column) and published half by half into the 16-row image; the next visit's
+    // loads are issued once the second half is published and land during its chunk's phases
+    // (a second register set -- 1.5 visits of cover -- pushed the kernel past the two waves
+    // per SIMD that its registers allow, or into scratch).
+    const long long nvis = (nchunks + 1) / 2;
+    const long long v0 = nvis * rng / nrng, v1 = nvis * (rng + 1) / nrng;
+    auto load = [&](d2(&pp)[NLD], long long v) __attribute__((always_inline)) {
+      const long long rv = (v < nvis ? v : nvis - 1) * VIS;
+#pragma unroll
+      for (int m = 0; m < NLD; ++m) pp[m] = *(const d2 *)(lsrc[m] + rv);
+    };
+    auto visit = [&](d2(&pp)[NLD], long long v, long long nxt) __attribute__((always_inline)) {
+      publish(pp, 0);
+      lds_barrier();
+      if (v < v1 && 2 * v < nchunks) compute(2 * v);
+      lds_barrier();
+      publish(pp, 1);
+      lds_barrier();
+      load(pp, nxt);
+      if (v < v1 && 2 * v + 1 < nchunks) compute(2 * v + 1);
+      lds_barrier();
+    };
+    d2 pa[NLD];
+    load(pa, v0);
+    for (long long v = v0; v < v1; ++v) visit(pa, v, v + 1);
+  } else {
   const long long cf = c0 < c1 ? c0 : nchunks - 1;  // empty range (k > 8, few chunks): any valid chunk
   {
     // 1-deep register prefetch: the next chunk's loads are issued right after the barrier
@@ -780,6 +822,7 @@ __global__ __launch_bounds__(NT) void k_nn_tn_w(MvDesc Q, int L, const double *_
     for (int m = 0; m < NLD; ++m) p[m] = *(const d2 *)(lsrc[m] + cf * RW);
     if ((NT_DIAG_MASK & 8) && ST) pout[0] = 0.0;
     for (long long ch = c0; ch < c1; ch += cstep) body(p, ch, ch + cstep);
+  }
   }
   // partial (L x k) of this workgroup: tile tt rows 16 tt + 4 b + m
   double *out = pout;
@@ -1044,16 +1087,16 @@ static nt_kernel_t nt_pick(int L, int k) {
 constexpr int NW_RW = NT_WIDE_RW;  // rows per chunk of the wide variant (32: 2 WGs/CU, 64: 1 WG/CU)
 constexpr int NW_WG_PER_CU = NT_WIDE_WGCU;
 
-template <int RW, int NJ, bool ST, int NT = 16 * RW>
+template <int RW, int NJ, bool ST, int NT = 16 * RW, int VIS = RW>
 static nt_kernel_t nw_pick_nm(int LX) {
   switch ((LX + 31) >> 5) {
 #define NW_CASE(N) \
   case N:          \
-    return k_nn_tn_w<RW, N, NJ, ST, NT>;
+    return k_nn_tn_w<RW, N, NJ, ST, NT, VIS>;
     NW_CASE(1) NW_CASE(2) NW_CASE(3) NW_CASE(4) NW_CASE(5) NW_CASE(6) NW_CASE(7) NW_CASE(8)
     NW_CASE(9) NW_CASE(10) NW_CASE(11) NW_CASE(12) NW_CASE(13) NW_CASE(14) NW_CASE(15)
 #undef NW_CASE
-    default: return k_nn_tn_w<RW, 16, NJ, ST, NT>;
+    default: return k_nn_tn_w<RW, 16, NJ, ST, NT, VIS>;
   }
 }
 
@@ -1102,6 +1145,18 @@ static int nw16_threads(int L, int k) {
   if (m == 3) return 512;
   if (m == 1 && (160 * 1024) / nw_lds_bytes<NW_RW>(L, 4) == 0) return 512;
   return 256;
+}
+// 16-row workgroups (256 threads) read 32-row visits (k_nn_tn_w VIS = 32): MIGMRES_NT_VIS32=1.
+// Off by default: measured slower at k = 16 (tools/mb_k16.cpp, same box: L = 224 8.45 vs
+// 7.99 ms, L = 256 9.49 vs 8.82; profiles/r3_k16_nntn_vis32.txt) -- the wider visits do not
+// make up for the loads' shorter cover (issued after the second half is published).
+static bool nw16_vis32() {
+  static int v = -1;
+  if (v < 0) {
+    const char *e = std::getenv("MIGMRES_NT_VIS32");
+    v = e ? std::atoi(e) : 0;
+  }
+  return v != 0;
 }
 static int nw16_per_cu(int L, int k) { return nw16_threads(L, k) == 512 ? nw16_occ<512>(L, k) : nw16_occ<256>(L, k); }
 static int nw_rw(int L, int k) {
@@ -1202,13 +1257,20 @@ void launch_nn_tn(hipStream_t s, MvDesc Q, int L, const double *C1, int ldc, MvD
     const int kh = paired ? 8 : k;
     if (nw_rw(L, k) == 16) {
       const bool t512 = nw16_threads(L, k) == 512;
-      nt_kernel_t f = t512 ? nw_pick_nm<16, 4, false, 512>(L + kh) : nw_pick_nm<16, 4, false>(L + kh);
-      static bool attr16[2][17] = {};
+      // 32-row visits where C1 is in LDS anyway (images past 7 x 32 columns): same LDS and
+      // occupancy as the 16-row visit form
+      // (up to 10 x 32 columns: two waves per SIMD still fit its registers)
+      const bool v32 = !t512 && nw16_vis32() && ((L + kh + 31) >> 5) > 7 && ((L + kh + 31) >> 5) <= 10;
+      nt_kernel_t f = t512 ? nw_pick_nm<16, 4, false, 512>(L + kh)
+                      : v32 ? nw_pick_nm<16, 4, false, 256, 32>(L + kh)
+                            : nw_pick_nm<16, 4, false>(L + kh);
+      static bool attr16[3][17] = {};
       const int nm = (L + kh + 31) >> 5;
-      if (!attr16[t512][nm]) {
+      const int fv = t512 ? 1 : v32 ? 2 : 0;
+      if (!attr16[fv][nm]) {
         if (hipFuncSetAttribute((const void *)f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
           throw Error(MIGMRES_EHIP, "nn_tn: cannot raise the dynamic LDS limit");
-        attr16[t512][nm] = true;
+        attr16[fv][nm] = true;
       }
       const size_t lds16 = t512 ? nw_lds_bytes<16, 512>(L, 4, L + kh) : nw_lds_bytes<16>(L, 4, L + kh);
       hipLaunchKernelGGL(f, dim3(nblocks), dim3(t512 ? 512 : 256), lds16, s, Q, L, C1, ldc, X, k, nrows,
