@@ -260,6 +260,28 @@ int migmres_dgks_normalize(migmres_mv *X, double *B, int ldb, int *rank);
  * solution (ifpack2/src/Ifpack2_Relaxation_def.hpp:1390-1454 ApplyInverseJacobi; the
  * inverse diagonal as compute() :1240-1270).  A must outlive the preconditioner. */
 int migmres_jacobi_create(migmres_crs *A, int sweeps, double damping, migmres_prec **out);
+/* The full Ifpack2::Relaxation parameter list the device path implements
+ * (Ifpack2_Relaxation_def.hpp:243-307 names and defaults, compute() :990-1320, apply
+ * :1323-1454): "relaxation: type" Jacobi (0) or Richardson (1), "sweeps", "damping factor",
+ * "zero starting solution" (0: apply starts from Y's contents), "use l1" with "l1 eta" (on more
+ * than one process: d_i += sum of |a_ij / 2| over the off-process columns whose local index
+ * exceeds the local row count, when |d_i| < eta times that sum), "min diagonal value" and
+ * "fix tiny diagonal entries" (|d_i| <= |min| -> 1 / min, 1 / eps for min = 0), "check diagonal
+ * entries" (statistics only).  migmres_jacobi_create(A, s, w, &M) = these defaults with sweeps
+ * s and damping w. */
+typedef struct migmres_relaxation_params {
+  int type;                      /* 0 "Jacobi" (default), 1 "Richardson" */
+  int sweeps;                    /* 1 */
+  double damping;                /* 1.0 */
+  int zero_starting_solution;    /* 1 */
+  int use_l1;                    /* 0 */
+  double l1_eta;                 /* 1.5 */
+  double min_diagonal_value;     /* 0.0 */
+  int fix_tiny_diagonal_entries; /* 0 */
+  int check_diagonal_entries;    /* 0 */
+} migmres_relaxation_params;
+int migmres_relaxation_params_default(migmres_relaxation_params *p);
+int migmres_relaxation_create(migmres_crs *A, const migmres_relaxation_params *p, migmres_prec **out);
 int migmres_prec_destroy(migmres_prec *M);
 /* Y = M X (Ifpack2::Relaxation::apply / Ifpack2::Chebyshev::apply, alpha = 1, beta = 0).
  * X may alias Y (apply(x, x)): M then reads a deep copy of X, as

@@ -64,6 +64,83 @@ class Jacobi:
 
 
 # ---------------------------------------------------------------------------------------
+# Ifpack2::Relaxation's full option set for the types on the device path
+# (Ifpack2_Relaxation_def.hpp: defaults :243-307, compute() :990-1280, apply :1323-1454).
+# ---------------------------------------------------------------------------------------
+
+RELAXATION_DEFAULTS = {
+    "relaxation: type": "Jacobi", "relaxation: sweeps": 1, "relaxation: damping factor": 1.0,
+    "relaxation: zero starting solution": True, "relaxation: use l1": False, "relaxation: l1 eta": 1.5,
+    "relaxation: min diagonal value": 0.0, "relaxation: fix tiny diagonal entries": False,
+    "relaxation: check diagonal entries": False,
+}
+
+
+def relaxation_inverse_diagonal(A, params):
+    """compute()'s inverse diagonal over a DistCrs `A` (global vector).  Per rank, from its
+    local CRS (local column ids, owned columns first): the first entry with local column ==
+    row; with "use l1" on more than one rank, boost = sum of |v / 2| over the entries whose
+    local column index exceeds the local row count (:1070-1081, the reference's `>`), added
+    when |d| < eta * boost; then 1 / d, or with "fix tiny diagonal entries" 1 / min (1 / eps
+    for min = 0) where |d| <= |min| (:1247-1274)."""
+    p = dict(RELAXATION_DEFAULTS)
+    p.update(params)
+    out = np.zeros(A.n_global)
+    eps = float(np.finfo(np.float64).eps)
+    for q in range(A.nprocs):
+        rp, lc, vv = A.crs[q]
+        f, nl = A.firsts[q], A.nlocs[q]
+        cm = A.colmaps[q]
+        for i in range(nl):
+            d = 0.0
+            for e in range(int(rp[i]), int(rp[i + 1])):
+                if cm[lc[e]] == f + i:
+                    d = vv[e]
+                    break
+            if p["relaxation: use l1"] and A.nprocs > 1:
+                boost = 0.0
+                for e in range(int(rp[i]), int(rp[i + 1])):
+                    if lc[e] > nl:
+                        boost += abs(vv[e] / 2.0)
+                if abs(d) < p["relaxation: l1 eta"] * boost:
+                    d += boost
+            mn = float(p["relaxation: min diagonal value"])
+            if p["relaxation: fix tiny diagonal entries"] and abs(d) <= abs(mn):
+                out[f + i] = 1.0 / eps if mn == 0.0 else 1.0 / mn
+            else:
+                with np.errstate(divide="ignore"):
+                    out[f + i] = 1.0 / d
+    return out
+
+
+class Relaxation:
+    """Y = M X for Ifpack2::Relaxation "Jacobi" or "Richardson" with any sweeps, damping and
+    start (Y0 = the initial Y when "zero starting solution" is false)."""
+
+    def __init__(self, A, params):
+        p = dict(RELAXATION_DEFAULTS)
+        p.update(params)
+        self.p, self.A = p, A
+        self.dinv = relaxation_inverse_diagonal(A, p)
+        self.n_apply = 0
+
+    def __call__(self, X, Y0=None):
+        self.n_apply += 1
+        p = self.p
+        X = np.asarray(X, dtype=np.float64)
+        om = float(p["relaxation: damping factor"])
+        jac = p["relaxation: type"] == "Jacobi"
+        ab = (om * self.dinv)[:, None]
+        zero = p["relaxation: zero starting solution"]
+        Y = np.zeros_like(X) if Y0 is None else np.array(Y0, dtype=np.float64)
+        if zero:
+            Y = ab * X if jac else om * X
+        for _ in range(1 if zero else 0, int(p["relaxation: sweeps"])):
+            R = X - self.A.apply(Y)
+            Y = 1.0 * Y + ab * R if jac else om * R + 1.0 * Y
+        return Y
+
+# ---------------------------------------------------------------------------------------
 # Ifpack2::Chebyshev (ifpack2/src/Ifpack2_Chebyshev_def.hpp over
 # Ifpack2_Details_Chebyshev_def.hpp), the smoother of SURVEY 8(f) rank 2.
 #   parameters (Details::Chebyshev :280-300 defaults, setParameters :333-677): "chebyshev:

@@ -86,6 +86,8 @@ _SIGS = {
     "migmres_prec_apply": [vp, vp, vp],
     "migmres_prec_diagonal": [vp, P(f64)],
     "migmres_chebyshev_params_default": [vp],
+    "migmres_relaxation_params_default": [vp],
+    "migmres_relaxation_create": [vp, vp, P(vp)],
     "migmres_crs_format_digest": [vp, P(C.c_ulonglong), i32, P(i32)],
     "migmres_chebyshev_create": [vp, vp, P(vp)],
     "migmres_chebyshev_lambdas": [vp, P(f64), P(f64), P(f64)],

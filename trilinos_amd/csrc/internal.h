@@ -149,6 +149,9 @@ void launch_diag_inv(hipStream_t s, const int *rowptr, const int *cols, const do
                      double *dinv);
 void launch_jacobi(hipStream_t s, MvDesc X, MvDesc Y, const double *dinv, double omega, int nrows,
                    bool accumulate);
+// Ifpack2::Relaxation's inverse diagonal with the l1 and fix-tiny options (kernels.hip).
+void launch_relax_diag(hipStream_t s, const int *rowptr, const int *cols, const double *vals, int n, int n_present,
+                       bool l1, double eta, bool fix_tiny, double min_val, double *dinv);
 // Ifpack2::Chebyshev: dinv = reciprocal_threshold(diag, min_val); the ChebyshevKernel step
 // W = [beta W +] (alpha dinv) R, X = X + W (xmode 1) / X = W (2) / untouched (0); Y = a A + b B
 // without contraction.

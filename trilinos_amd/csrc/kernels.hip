@@ -1553,6 +1553,38 @@ __global__ __launch_bounds__(256) void k_jacobi(MvDesc X, MvDesc Y, const double
   *y = ACC ? 1.0 * (*y) + t : t;
 }
 
+// Ifpack2::Relaxation::compute()'s inverse diagonal (Ifpack2_Relaxation_def.hpp:990-1280):
+// the diagonal copy; with l1 (more than one process) d += boost = sum of |a / 2| over the
+// entries whose local column index exceeds the local row count (the reference's `>`: the
+// first ghost column does not count; a ghost's index is n_present + its slot), when |d| <
+// eta boost; then 1 / d, or with fix_tiny 1 / min (1 / eps for min = 0) where |d| <= |min|.
+__global__ __launch_bounds__(256) void k_relax_diag(const int *__restrict__ rowptr, const int *__restrict__ cols,
+                                                    const double *__restrict__ vals, int n, int n_present, int l1,
+                                                    double eta, int fix_tiny, double min_val,
+                                                    double *__restrict__ dinv) {
+#pragma clang fp contract(off)
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= n) return;
+  double d = 0.0;
+  for (int p = rowptr[r]; p < rowptr[r + 1]; ++p)
+    if (cols[p] == r) {
+      d = vals[p];
+      break;
+    }
+  if (l1) {
+    double boost = 0.0;
+    for (int p = rowptr[r]; p < rowptr[r + 1]; ++p) {
+      const int c = cols[p];
+      if (c >= n && (long long)n_present + (c - n) > n) boost += fabs(vals[p] / 2.0);
+    }
+    if (fabs(d) < eta * boost) d += boost;
+  }
+  if (fix_tiny && fabs(d) <= fabs(min_val))
+    dinv[r] = min_val == 0.0 ? 1.0 / 2.220446049250313e-16 : 1.0 / min_val;
+  else
+    dinv[r] = 1.0 / d;
+}
+
 // Ifpack2::Chebyshev's inverse diagonal: reciprocal_threshold of the diagonal copy
 // (Ifpack2_Details_Chebyshev_def.hpp:104-115): |d| < |min_val| stores min_val itself.
 __global__ __launch_bounds__(256) void k_diag_recip_threshold(const int *__restrict__ rowptr,
@@ -1627,6 +1659,13 @@ void launch_diag_inv(hipStream_t s, const int *rowptr, const int *cols, const do
                      double *dinv) {
   if (n <= 0) return;
   k_diag_inv<<<cdiv(n, 256), 256, 0, s>>>(rowptr, cols, vals, n, dinv);
+  LAUNCH_CHECK();
+}
+void launch_relax_diag(hipStream_t s, const int *rowptr, const int *cols, const double *vals, int n, int n_present,
+                       bool l1, double eta, bool fix_tiny, double min_val, double *dinv) {
+  if (n <= 0) return;
+  k_relax_diag<<<cdiv(n, 256), 256, 0, s>>>(rowptr, cols, vals, n, n_present, l1 ? 1 : 0, eta, fix_tiny ? 1 : 0,
+                                            min_val, dinv);
   LAUNCH_CHECK();
 }
 void launch_diag_recip_threshold(hipStream_t s, const int *rowptr, const int *cols, const double *vals, int n,

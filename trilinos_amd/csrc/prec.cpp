@@ -185,20 +185,27 @@ void prec_apply(migmres_prec &M, const migmres_mv &X_in, migmres_mv &Y) {
     ++M.n_apply;
     return;
   }
-  {
+  // ApplyInverseJacobi / ApplyInverseRichardson (Ifpack2_Relaxation_def.hpp:1323-1454)
+  const bool jacobi = M.rtype == 0;
+  if (M.zero_start) {  // first sweep from Y = 0: Y = (omega d^-1) X, or Y = omega X
     ProfScope ps(c, K_AXPBY, 8.0 * n * (2.0 * X.ncols + 1.0));
-    launch_jacobi(c->stream, X.desc(), Y.desc(), M.d_dinv, M.damping, n, false);
-  }
-  if (M.sweeps > 1) {
-    if (!M.work || M.work->ncols != X.ncols) {
-      delete M.work;
-      M.work = mv_create(c, X.n_global, X.n_local, X.ncols);
+    if (jacobi) {
+      launch_jacobi(c->stream, X.desc(), Y.desc(), M.d_dinv, M.damping, n, false);
+    } else {
+      mv_assign(X, Y);
+      mv_scale(Y, M.damping);
     }
-    for (int j = 1; j < M.sweeps; ++j) {
-      mv_assign(X, *M.work);
-      crs_apply(*M.A, Y, *M.work, -1.0, 1.0);
+  }
+  const int start = M.zero_start ? 1 : 0;
+  if (M.sweeps > start) {
+    migmres_mv &R = scratch(M.work, X);
+    for (int j = start; j < M.sweeps; ++j) {
+      residual(M, X, Y, R);  // R = X - A Y
       ProfScope ps(c, K_AXPBY, 8.0 * n * (3.0 * X.ncols + 1.0));
-      launch_jacobi(c->stream, M.work->desc(), Y.desc(), M.d_dinv, M.damping, n, true);
+      if (jacobi)  // Y = 1*Y + (omega d^-1) R
+        launch_jacobi(c->stream, R.desc(), Y.desc(), M.d_dinv, M.damping, n, true);
+      else  // Y.update(omega, R, 1): omega R + 1 Y
+        launch_lincomb(c->stream, M.damping, R.desc(), 1.0, Y.desc(), Y.desc(), n);
     }
   }
   ++M.n_apply;
@@ -206,26 +213,62 @@ void prec_apply(migmres_prec &M, const migmres_mv &X_in, migmres_mv &Y) {
 
 }  // namespace migmres
 
-extern "C" int migmres_jacobi_create(migmres_crs *A, int sweeps, double damping, migmres_prec **out) {
+extern "C" int migmres_relaxation_params_default(migmres_relaxation_params *p) {
   return guard([&] {
-    MIG_CHECK(A && out, "jacobi_create: null argument");
-    MIG_CHECK(sweeps >= 1, "\"relaxation: sweeps\" must be >= 1");
-    auto *M = new migmres_prec();
+    MIG_CHECK(p, "relaxation_params_default: null argument");
+    *p = migmres_relaxation_params{};
+    p->type = 0;
+    p->sweeps = 1;
+    p->damping = 1.0;
+    p->zero_starting_solution = 1;
+    p->use_l1 = 0;
+    p->l1_eta = 1.5;
+    p->min_diagonal_value = 0.0;
+    p->fix_tiny_diagonal_entries = 0;
+    p->check_diagonal_entries = 0;
+  });
+}
+
+extern "C" int migmres_relaxation_create(migmres_crs *A, const migmres_relaxation_params *p, migmres_prec **out) {
+  return guard([&] {
+    MIG_CHECK(A && p && out, "relaxation_create: null argument");
+    MIG_CHECK(p->type == 0 || p->type == 1, "\"relaxation: type\": the device path implements Jacobi and Richardson");
+    MIG_CHECK(p->sweeps >= 0, "\"relaxation: sweeps\" must be nonnegative");
+    std::unique_ptr<migmres_prec> M(new migmres_prec());
     M->ctx = A->ctx;
     M->A = A;
-    M->sweeps = sweeps;
-    M->damping = damping;
+    M->rtype = p->type;
+    M->sweeps = p->sweeps;
+    M->damping = p->damping;
+    M->zero_start = p->zero_starting_solution != 0;
     const int n = A->n_local;
+    const int n_present = A->n_cols - (int)A->plan.remote_lids.size();
     MIG_HIP(hipMalloc(&M->d_dinv, sizeof(double) * (n > 0 ? n : 1)));
-    launch_diag_inv(A->ctx->stream, A->d_rowptr, A->d_cols, A->d_vals, n, M->d_dinv);
+    // IsParallel_: the l1 boost only on more than one process (Ifpack2_Relaxation_def.hpp:1052)
+    launch_relax_diag(A->ctx->stream, A->d_rowptr, A->d_cols, A->d_vals, n, n_present,
+                      p->use_l1 && A->ctx->nranks > 1, p->l1_eta, p->fix_tiny_diagonal_entries != 0,
+                      p->min_diagonal_value, M->d_dinv);
     // the fused form's column scale omega * dinv, with two zero entries past n for the row-pair
     // kernels' reads of a last half-filled pair
     MIG_HIP(hipMalloc(&M->d_sdinv, sizeof(double) * ((size_t)n + 2)));
     MIG_HIP(hipMemsetAsync(M->d_sdinv, 0, sizeof(double) * ((size_t)n + 2), A->ctx->stream));
-    launch_scaled_copy(A->ctx->stream, M->d_dinv, damping, M->d_sdinv, n);
+    launch_scaled_copy(A->ctx->stream, M->d_dinv, p->damping, M->d_sdinv, n);
     MIG_HIP(hipStreamSynchronize(A->ctx->stream));
-    if (sweeps == 1) prec_import_ghost_scale(*M);  // the fused form's ghost column scale
-    *out = M;
+    // the fused right Jacobi (one zero-start Jacobi sweep) and its ghost column scale
+    if (M->rtype == 0 && M->sweeps == 1 && M->zero_start) prec_import_ghost_scale(*M);
+    *out = M.release();
+  });
+}
+
+extern "C" int migmres_jacobi_create(migmres_crs *A, int sweeps, double damping, migmres_prec **out) {
+  return guard([&] {
+    MIG_CHECK(sweeps >= 1, "\"relaxation: sweeps\" must be >= 1");
+    migmres_relaxation_params p;
+    migmres_relaxation_params_default(&p);
+    p.sweeps = sweeps;
+    p.damping = damping;
+    const int rc = migmres_relaxation_create(A, &p, out);
+    if (rc != MIGMRES_OK) throw Error(rc, migmres_last_error());
   });
 }
 

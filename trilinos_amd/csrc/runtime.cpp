@@ -1227,7 +1227,7 @@ bool crs_apply_jacobi_fused(migmres_crs &A, const migmres_prec &M, const migmres
   const int n_remote = (int)A.plan.remote_lids.size();
   const int n_export = (int)A.export_lids.size();
   const bool halo = c->dist && (n_remote > 0 || n_export > 0);
-  if (M.kind != 0 || M.sweeps != 1 || !M.d_sdinv || M.A != &A) return false;
+  if (M.kind != 0 || M.rtype != 0 || !M.zero_start || M.sweeps != 1 || !M.d_sdinv || M.A != &A) return false;
   if (halo && n_remote > 0 && !M.d_gsdinv) return false;
   if (X.n_local != A.n_local || Y.n_local != A.n_local || X.ncols != Y.ncols) return false;
   crs_apply_impl(A, X, Y, 1.0, 0.0, ColScale{M.d_sdinv, M.d_gsdinv});

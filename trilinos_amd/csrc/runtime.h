@@ -202,6 +202,8 @@ struct migmres_prec {
   migmres_mv *xcopy = nullptr;  // deep copy of X when apply(X, Y) aliases
   // kind 1: Ifpack2::Chebyshev (prec.cpp); d_dinv holds the reciprocal_threshold diagonal
   int kind = 0;
+  int rtype = 0;            // kind 0: 0 Jacobi, 1 Richardson (no diagonal)
+  bool zero_start = true;   // "relaxation: zero starting solution"
   migmres_chebyshev_params cheb{};
   double cheb_computed_lmax = 0.0, cheb_lmax = 0.0, cheb_lmin = 0.0, cheb_ratio = 0.0;
   migmres_mv *cheb_w = nullptr, *cheb_p = nullptr;  // W (and the textbook form's P)

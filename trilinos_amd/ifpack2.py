@@ -12,20 +12,33 @@ import numpy as np
 
 from ._lib import call, dptr
 
-# Ifpack2_Relaxation_def.hpp:264-300 (the subset the device path implements)
+# Ifpack2_Relaxation_def.hpp:243-307 (the parameters of the types the device path implements)
 DEFAULT_PARAMETERS = {
     "relaxation: type": "Jacobi",
     "relaxation: sweeps": 1,
     "relaxation: damping factor": 1.0,
     "relaxation: zero starting solution": True,
     "relaxation: use l1": False,
+    "relaxation: l1 eta": 1.5,
+    "relaxation: min diagonal value": 0.0,
     "relaxation: fix tiny diagonal entries": False,
     "relaxation: check diagonal entries": False,
 }
+RELAXATION_TYPES = {"Jacobi": 0, "Richardson": 1}
+
+
+class _RelaxParams(C.Structure):
+    """migmres_relaxation_params (include/migmres.h)."""
+    _fields_ = [("type", C.c_int), ("sweeps", C.c_int), ("damping", C.c_double),
+                ("zero_starting_solution", C.c_int), ("use_l1", C.c_int), ("l1_eta", C.c_double),
+                ("min_diagonal_value", C.c_double), ("fix_tiny_diagonal_entries", C.c_int),
+                ("check_diagonal_entries", C.c_int)]
 
 
 class Relaxation:
-    """Ifpack2::Relaxation<CrsMatrix>: setParameters -> initialize -> compute -> apply."""
+    """Ifpack2::Relaxation<CrsMatrix>: setParameters -> initialize -> compute -> apply.
+    "relaxation: type" "Jacobi" or "Richardson" (the Gauss-Seidel family is sequential and not
+    on the device path)."""
 
     def __init__(self, A):
         self.A = A
@@ -39,16 +52,10 @@ class Relaxation:
                 raise KeyError(f'"{k}" is not a valid Ifpack2::Relaxation parameter for the device path')
             self.params[k] = v
         p = self.params
-        if p["relaxation: type"] != "Jacobi":
-            raise NotImplementedError('the device path implements "relaxation: type" = "Jacobi"')
+        if p["relaxation: type"] not in RELAXATION_TYPES:
+            raise NotImplementedError('the device path implements "relaxation: type" = "Jacobi" and "Richardson"')
         if int(p["relaxation: sweeps"]) < 0:
             raise ValueError('"relaxation: sweeps" must be nonnegative')
-        if not p["relaxation: zero starting solution"]:
-            raise NotImplementedError('"relaxation: zero starting solution" = false is not implemented')
-        for k in ("relaxation: use l1", "relaxation: fix tiny diagonal entries",
-                  "relaxation: check diagonal entries"):
-            if p[k]:
-                raise NotImplementedError(f'"{k}" = true is not implemented')
 
     def initialize(self):
         self._initialized = True
@@ -57,13 +64,24 @@ class Relaxation:
         return self._initialized
 
     def compute(self):
-        """Extract and invert the diagonal on the device."""
+        """Extract and invert the diagonal on the device (l1 / fix-tiny options applied)."""
         if not self._initialized:
             self.initialize()
         self._free()
+        p = self.params
+        cp = _RelaxParams()
+        call("migmres_relaxation_params_default", C.byref(cp))
+        cp.type = RELAXATION_TYPES[p["relaxation: type"]]
+        cp.sweeps = int(p["relaxation: sweeps"])
+        cp.damping = float(p["relaxation: damping factor"])
+        cp.zero_starting_solution = 1 if p["relaxation: zero starting solution"] else 0
+        cp.use_l1 = 1 if p["relaxation: use l1"] else 0
+        cp.l1_eta = float(p["relaxation: l1 eta"])
+        cp.min_diagonal_value = float(p["relaxation: min diagonal value"])
+        cp.fix_tiny_diagonal_entries = 1 if p["relaxation: fix tiny diagonal entries"] else 0
+        cp.check_diagonal_entries = 1 if p["relaxation: check diagonal entries"] else 0
         h = C.c_void_p()
-        call("migmres_jacobi_create", self.A.h, int(self.params["relaxation: sweeps"]),
-             float(self.params["relaxation: damping factor"]), C.byref(h))
+        call("migmres_relaxation_create", self.A.h, C.byref(cp), C.byref(h))
         self.h = h
 
     def isComputed(self):
@@ -71,7 +89,8 @@ class Relaxation:
 
     def apply(self, X, Y, alpha=1.0, beta=0.0):
         """Y = alpha M X (Ifpack2_Relaxation_def.hpp:494-592): beta != 0 is rejected as in the
-        reference, alpha == 0 zeroes Y, X may be Y (the sweeps then read a copy of X)."""
+        reference, alpha == 0 zeroes Y, X may be Y (the sweeps then read a copy of X); with
+        "zero starting solution" false the sweeps start from Y's contents."""
         if self.h is None:
             raise RuntimeError("Ifpack2::Relaxation::apply: compute() has not been called")
         if X.ncols != Y.ncols:
