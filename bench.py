@@ -202,6 +202,10 @@ def main():
                          "image) read natively by every rank; overrides --matrix/--nx")
     ap.add_argument("--prec", default="none", choices=["none", "right", "left"])
     ap.add_argument("--sweeps", type=int, default=1)
+    ap.add_argument("--prec-type", default="jacobi", choices=["jacobi", "chebyshev"],
+                    help="the --prec preconditioner: Ifpack2::Relaxation Jacobi (--sweeps) or Ifpack2::Chebyshev "
+                         "(--cheb-degree, power-method lambda max)")
+    ap.add_argument("--cheb-degree", type=int, default=3)
     ap.add_argument("--ortho", default="ICGS", choices=["ICGS", "DGKS"])
     ap.add_argument("--comm-timeout", type=float, default=300.0,
                     help="seconds: torch.distributed (gloo) set-up / barrier timeout and the RCCL init watchdog")
@@ -254,8 +258,12 @@ def main():
         A = ta.CrsMatrix.galeri(comm, args.matrix, nx, nx, nx)
     M = None
     if args.prec != "none":
-        M = ta.Relaxation(A)
-        M.setParameters({"relaxation: sweeps": args.sweeps})
+        if args.prec_type == "chebyshev":
+            M = ta.Chebyshev(A)
+            M.setParameters({"chebyshev: degree": args.cheb_degree})
+        else:
+            M = ta.Relaxation(A)
+            M.setParameters({"relaxation: sweeps": args.sweeps})
         M.compute()
     Xex = ta.MultiVector(comm, n, k)
     Xex.random(1)
@@ -327,8 +335,9 @@ def main():
              f"{args.matrix} n={nx}^3")
     wl = (f"3-D 7-pt Laplacian n={nx}^3 fp64, k={k} RHS, Block GMRES Num Blocks {nb}, ICGS, fixed work (tol 0)"
           if headline else
-          f"{mname} fp64, k={k} RHS, {args.solver} Num Blocks {nb}, {args.ortho}, "
-          f"Jacobi({args.sweeps} sweeps) {args.prec} preconditioner, fixed work (tol 0)"
+          f"{mname} fp64, k={k} RHS, {args.solver} Num Blocks {nb}, {args.ortho}, " +
+          (f"Chebyshev(degree {args.cheb_degree}) " if args.prec_type == "chebyshev" else
+           f"Jacobi({args.sweeps} sweeps) ") + f"{args.prec} preconditioner, fixed work (tol 0)"
           if args.prec != "none" else
           f"{mname} fp64, k={k} RHS, {args.solver} Num Blocks {nb}, {args.ortho}, fixed work (tol 0)")
     out = {

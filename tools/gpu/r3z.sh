@@ -1,0 +1,6 @@
+source ./tools/gpu/step.sh
+P=${PROF:-r3z}
+
+step 400 bench_cheb_$P.json python bench.py --no-cpu-baseline --matrix Brick3D --prec right --prec-type chebyshev --cheb-degree 3
+tail -1 gpurun_out/bench_128_$P.json | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('128^3', d['value'], d['ms_per_step']); print({k:(round(v['ms'],1),v['launches']) for k,v in d['kernels'].items()})"
+tail -1 gpurun_out/bench_cheb_$P.json | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('cheb', d['value'], d['ms_per_step']); print({k:(round(v['ms'],1),v['launches']) for k,v in d['kernels'].items()})"

@@ -157,8 +157,9 @@ void launch_relax_diag(hipStream_t s, const int *rowptr, const int *cols, const 
 // without contraction.
 void launch_diag_recip_threshold(hipStream_t s, const int *rowptr, const int *cols, const double *vals, int n,
                                  double min_val, double *dinv);
-void launch_cheb_update(hipStream_t s, MvDesc R, MvDesc W, MvDesc X, const double *dinv, double alpha, double beta,
-                        bool use_beta, int xmode, int nrows);
+// (B.base != null: R holds A X and the kernel forms b - (A X) itself)
+void launch_cheb_update(hipStream_t s, MvDesc B, MvDesc R, MvDesc W, MvDesc X, const double *dinv, double alpha,
+                        double beta, bool use_beta, int xmode, int nrows);
 void launch_lincomb(hipStream_t s, double a, MvDesc A, double b, MvDesc B, MvDesc Y, int nrows);
 void launch_abs(hipStream_t s, MvDesc Y, int nrows);  // Y = |Y| (negative entries negated)
 // Import exchange layout [neighbour][column][count] (grp[i] = (offset, count) of entry i's

@@ -1606,14 +1606,18 @@ __global__ __launch_bounds__(256) void k_diag_recip_threshold(const int *__restr
 // residual R = B - A X formed by the SpMM: W = beta W + (alpha d_i) R (BETA) or
 // W = (alpha d_i) R, then X = X + W (XMODE 1), X = W (XMODE 2, the zero-start first step)
 // or X untouched (XMODE 0); each product and sum rounded separately.
+// With B given (B.base != null) R holds A X and the residual b - (A X) is formed here: the
+// same bits as the SpMM's -1 * sum + 1 * b, without a copy of B.
 template <bool BETA, int XMODE>
-__global__ __launch_bounds__(256) void k_cheb_update(MvDesc R, MvDesc W, MvDesc X, const double *__restrict__ dinv,
-                                                     double alpha, double beta, int nrows) {
+__global__ __launch_bounds__(256) void k_cheb_update(MvDesc B, MvDesc R, MvDesc W, MvDesc X,
+                                                     const double *__restrict__ dinv, double alpha, double beta,
+                                                     int nrows) {
 #pragma clang fp contract(off)
   const int c = blockIdx.y;
   const long long r = (long long)blockIdx.x * 256 + threadIdx.x;
   if (r >= nrows) return;
-  const double t = (alpha * dinv[r]) * colp(R, c)[r];
+  const double res = B.base ? colp(B, c)[r] - colp(R, c)[r] : colp(R, c)[r];
+  const double t = (alpha * dinv[r]) * res;
   double *wp = colp(W, c) + r;
   const double w = BETA ? beta * (*wp) + t : t;
   *wp = w;
@@ -1674,18 +1678,18 @@ void launch_diag_recip_threshold(hipStream_t s, const int *rowptr, const int *co
   k_diag_recip_threshold<<<cdiv(n, 256), 256, 0, s>>>(rowptr, cols, vals, n, min_val, dinv);
   LAUNCH_CHECK();
 }
-void launch_cheb_update(hipStream_t s, MvDesc R, MvDesc W, MvDesc X, const double *dinv, double alpha, double beta,
-                        bool use_beta, int xmode, int nrows) {
+void launch_cheb_update(hipStream_t s, MvDesc B, MvDesc R, MvDesc W, MvDesc X, const double *dinv, double alpha,
+                        double beta, bool use_beta, int xmode, int nrows) {
   if (nrows <= 0 || W.ncols <= 0) return;
   const dim3 g(cdiv(nrows, 256), W.ncols);
   if (use_beta) {
-    if (xmode == 1) k_cheb_update<true, 1><<<g, 256, 0, s>>>(R, W, X, dinv, alpha, beta, nrows);
-    else if (xmode == 2) k_cheb_update<true, 2><<<g, 256, 0, s>>>(R, W, X, dinv, alpha, beta, nrows);
-    else k_cheb_update<true, 0><<<g, 256, 0, s>>>(R, W, X, dinv, alpha, beta, nrows);
+    if (xmode == 1) k_cheb_update<true, 1><<<g, 256, 0, s>>>(B, R, W, X, dinv, alpha, beta, nrows);
+    else if (xmode == 2) k_cheb_update<true, 2><<<g, 256, 0, s>>>(B, R, W, X, dinv, alpha, beta, nrows);
+    else k_cheb_update<true, 0><<<g, 256, 0, s>>>(B, R, W, X, dinv, alpha, beta, nrows);
   } else {
-    if (xmode == 1) k_cheb_update<false, 1><<<g, 256, 0, s>>>(R, W, X, dinv, alpha, beta, nrows);
-    else if (xmode == 2) k_cheb_update<false, 2><<<g, 256, 0, s>>>(R, W, X, dinv, alpha, beta, nrows);
-    else k_cheb_update<false, 0><<<g, 256, 0, s>>>(R, W, X, dinv, alpha, beta, nrows);
+    if (xmode == 1) k_cheb_update<false, 1><<<g, 256, 0, s>>>(B, R, W, X, dinv, alpha, beta, nrows);
+    else if (xmode == 2) k_cheb_update<false, 2><<<g, 256, 0, s>>>(B, R, W, X, dinv, alpha, beta, nrows);
+    else k_cheb_update<false, 0><<<g, 256, 0, s>>>(B, R, W, X, dinv, alpha, beta, nrows);
   }
   LAUNCH_CHECK();
 }
