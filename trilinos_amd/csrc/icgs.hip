@@ -196,6 +196,16 @@ void launch_reduce_small(hipStream_t s, const double *partial, int nblocks, int 
 // X = beta X + alpha A M (M device, L x kx, leading dim ldm) and, if dmode != 0, partials
 // of sum_r Xnew[r,c] * D[r,c] (dmode 1: D = Xnew, 2: D given).  Grid-stride over row pairs.
 // -------------------------------------------------------------------------------------
+// The closing updates' basis loads (each basis element is read once per pass): plain, or
+// non-temporal with -DNN_NT_LOAD=1 (an A/B knob, tools/mb_k16.cpp).
+#ifndef NN_NT_LOAD
+#define NN_NT_LOAD 0
+#endif
+__device__ __forceinline__ d2 nn_load(const d2 *p) {
+  if (NN_NT_LOAD) return __builtin_nontemporal_load(p);
+  return *p;
+}
+
 template <int KX>
 __global__ __launch_bounds__(ICNT) void k_gemm_nn_dot(MvDesc A, int L, const double *__restrict__ M,
                                                      int ldm, MvDesc X, int kx, int nrows,
@@ -226,7 +236,7 @@ __global__ __launch_bounds__(ICNT) void k_gemm_nn_dot(MvDesc A, int L, const dou
     for (; j + NB <= L; j += NB) {
       d2 v[NB];
 #pragma unroll
-      for (int u = 0; u < NB; ++u) v[u] = *(const d2 *)(colp_(A, j + u) + r);
+      for (int u = 0; u < NB; ++u) v[u] = nn_load((const d2 *)(colp_(A, j + u) + r));
 #pragma unroll
       for (int u = 0; u < NB; ++u) {
         const double *mrow = &Ms[(j + u) * KX];
@@ -1938,7 +1948,7 @@ __global__ __launch_bounds__(FBG_NT) void k_gemm_nn_gram(MvDesc A, int L, const 
     for (; j + NB <= L; j += NB) {
       d2 v[NB];
 #pragma unroll
-      for (int u = 0; u < NB; ++u) v[u] = *(const d2 *)(colp_(A, j + u) + r);
+      for (int u = 0; u < NB; ++u) v[u] = nn_load((const d2 *)(colp_(A, j + u) + r));
 #pragma unroll
       for (int u = 0; u < NB; ++u)
 #pragma unroll
