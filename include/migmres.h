@@ -199,6 +199,10 @@ int migmres_crs_apply(migmres_crs *A, const migmres_mv *X, migmres_mv *Y, double
  * column triples, e.g. 3-dof meshes), one thread per block row; the other rows through the
  * SELL kernel (MIGMRES_NO_BSR3=1 at creation keeps MIGMRES_SPMM_SELL). */
 #define MIGMRES_SPMM_BSR3 5
+/* MIGMRES_SPMM_MARCH: the stencil-group templates of a 3-D 7- or 27-point grid read as a 2.5-D
+ * march -- plane tiles staged once in LDS, every key an LDS read; same bits as the template
+ * kernels (MIGMRES_NO_MARCH=1 at creation keeps MIGMRES_SPMM_TPL / MIGMRES_SPMM_TPL3). */
+#define MIGMRES_SPMM_MARCH 6
 int migmres_crs_spmm_kernel(const migmres_crs *A, int *kind);
 /* Digests (64-bit hashes) of the SpMM format plans A holds -- flags, fixed bytes and every
  * format array -- into out[0 .. n); *needed = the digest count.  Test support: the device

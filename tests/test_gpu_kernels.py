@@ -292,13 +292,15 @@ def test_epetra_gemm_known_answers(comm, n):
 @pytest.mark.parametrize("dims,k", [((12, 11, 10), 8), ((16, 9, 7), 1), ((10, 10, 10), 3), ((14, 8, 6), 5),
                                     ((20, 6, 5), 16), ((8, 7, 9), 9), ((6, 5, 4), 2)])
 @pytest.mark.parametrize("alpha,beta", [(1.0, 0.0), (-1.0, 1.0), (0.5, -2.0)])
-def test_spmm_tpl3_lane_shared_bit_exact(comm, dims, k, alpha, beta):
-    """27-point Brick3D on even-nx grids takes the lane-shared stencil-group kernel (one X load
-    per x-neighbour triple, the neighbours' halves by DPP wave shifts; waves of 62 outputs, so
-    several waves and boundary pairs sit in every case): bit for bit against the oracle for
-    every column count (chunks of 8, odd remainders), and Y = alpha A X + beta Y."""
+def test_spmm_tpl3_lane_shared_bit_exact(comm, dims, k, alpha, beta, monkeypatch):
+    """27-point Brick3D on even-nx grids takes the lane-shared stencil-group kernel when the
+    plane march is off (one X load per x-neighbour triple, the neighbours' halves by DPP wave
+    shifts; waves of 62 outputs, so several waves and boundary pairs sit in every case): bit
+    for bit against the oracle for every column count (chunks of 8, odd remainders), and
+    Y = alpha A X + beta Y."""
     import trilinos_amd as ta
     from oracle import epetra as oe
+    monkeypatch.setenv("MIGMRES_NO_MARCH", "1")
     nx, ny, nz = dims
     n = nx * ny * nz
     A = ta.CrsMatrix.galeri(comm, "Brick3D", nx, ny, nz)
@@ -313,11 +315,14 @@ def test_spmm_tpl3_lane_shared_bit_exact(comm, dims, k, alpha, beta):
     assert np.array_equal(Yd.download(), want)
 
 
-def test_spmm_tpl3_odd_nx_falls_back(comm):
+def test_spmm_tpl3_odd_nx_falls_back(comm, monkeypatch):
     """An odd nx puts row pairs across grid lines: no x-neighbour triples, so the operator
-    keeps the plain template kernel (still bit-exact, test_spmm_kernel_choice_bit_exact)."""
+    keeps the plain template kernel (still bit-exact, test_spmm_kernel_choice_bit_exact); so
+    does the 7-point operator on an even grid when the plane march is off."""
     import trilinos_amd as ta
     assert ta.CrsMatrix.galeri(comm, "Brick3D", 13, 12, 11).spmm_kernel() == "tpl"
+    assert ta.CrsMatrix.galeri(comm, "Laplace3D", 13, 12, 12).spmm_kernel() == "tpl"
+    monkeypatch.setenv("MIGMRES_NO_MARCH", "1")
     assert ta.CrsMatrix.galeri(comm, "Laplace3D", 12, 12, 12).spmm_kernel() == "tpl"
 
 
@@ -328,6 +333,7 @@ def test_spmm_tpl3_seven_point_bit_exact(comm, dims, k, monkeypatch):
     import trilinos_amd as ta
     from oracle import epetra as oe
     monkeypatch.setenv("MIGMRES_TPL3_SHORT", "1")
+    monkeypatch.setenv("MIGMRES_NO_MARCH", "1")
     nx, ny, nz = dims
     n = nx * ny * nz
     A = ta.CrsMatrix.galeri(comm, "Laplace3D", nx, ny, nz)
@@ -394,3 +400,54 @@ def test_spmm_bsr3_detects_not_assumes(comm):
     Yd = ta.MultiVector(comm, n, k)
     A.apply(_upload(ta, comm, X), Yd)
     assert np.array_equal(Yd.download(), Aor.apply(X))
+
+
+@pytest.mark.parametrize("kind,dims,k", [("Laplace3D", (12, 11, 10), 8), ("Laplace3D", (16, 9, 7), 1),
+                                         ("Laplace3D", (130, 6, 5), 3), ("Laplace3D", (8, 7, 9), 9),
+                                         ("Laplace3D", (4, 3, 3), 2), ("Brick3D", (12, 11, 10), 8),
+                                         ("Brick3D", (20, 6, 5), 16), ("Brick3D", (134, 5, 4), 5),
+                                         ("Brick3D", (6, 5, 4), 2), ("Brick3D", (10, 10, 10), 3)])
+@pytest.mark.parametrize("alpha,beta", [(1.0, 0.0), (-1.0, 1.0), (0.5, -2.0)])
+def test_spmm_march_bit_exact(comm, kind, dims, k, alpha, beta):
+    """7- and 27-point operators on even-nx grids take the 2.5-D plane march (plane tiles of
+    64 pairs x 4 lines staged once in LDS; partial x tiles at nx = 130 / 134, partial line
+    tiles, a few planes, odd column counts): bit for bit against the oracle, and
+    Y = alpha A X + beta Y."""
+    import trilinos_amd as ta
+    from oracle import epetra as oe
+    nx, ny, nz = dims
+    n = nx * ny * nz
+    A = ta.CrsMatrix.galeri(comm, kind, nx, ny, nz)
+    assert A.spmm_kernel() == "march"
+    gen = (lambda f, m: oe.brick3d_rows(nx, ny, nz, f, m)) if kind == "Brick3D" else \
+        (lambda f, m: oe.laplace3d_rows(nx, ny, nz, f, m))
+    Aor = oe.DistCrs(gen, n, 1)
+    X, _ = oe.epetra_random_mv(29, n, k)
+    Y0, _ = oe.epetra_random_mv(31, n, k)
+    Yd = _upload(ta, comm, Y0)
+    A.apply(_upload(ta, comm, X), Yd, alpha, beta)
+    want = alpha * Aor.apply(X) if beta == 0.0 else alpha * Aor.apply(X) + beta * Y0
+    assert np.array_equal(Yd.download(), want)
+
+
+@pytest.mark.parametrize("kc,sz", [("1", "1"), ("1", "3"), ("2", "2"), ("2", "5"), ("2", "64")])
+@pytest.mark.parametrize("kind", ["Laplace3D", "Brick3D"])
+def test_spmm_march_slabs_bit_exact(comm, kind, kc, sz, monkeypatch):
+    """The march's slab and column-chunk knobs (MIGMRES_MARCH_SZ planes per workgroup -- one
+    plane, ragged last slabs, one slab for all -- and MIGMRES_MARCH_KC columns per staged plane)
+    change only the walk: same bits as the oracle."""
+    import trilinos_amd as ta
+    from oracle import epetra as oe
+    monkeypatch.setenv("MIGMRES_MARCH_KC", kc)
+    monkeypatch.setenv("MIGMRES_MARCH_SZ", sz)
+    nx, ny, nz, k = 14, 9, 11, 5
+    n = nx * ny * nz
+    A = ta.CrsMatrix.galeri(comm, kind, nx, ny, nz)
+    assert A.spmm_kernel() == "march"
+    gen = (lambda f, m: oe.brick3d_rows(nx, ny, nz, f, m)) if kind == "Brick3D" else \
+        (lambda f, m: oe.laplace3d_rows(nx, ny, nz, f, m))
+    X, _ = oe.epetra_random_mv(37, n, k)
+    Yd = ta.MultiVector(comm, n, k)
+    A.apply(_upload(ta, comm, X), Yd)
+    assert np.array_equal(Yd.download(), oe.DistCrs(gen, n, 1).apply(X))
+

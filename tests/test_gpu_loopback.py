@@ -204,3 +204,35 @@ def test_ranks_without_rows(kind, dims, k, P):
     rel = np.linalg.norm(Bh - Aor.apply(X), axis=0) / np.linalg.norm(Bh, axis=0)
     rel_ref = np.linalg.norm(Bh - Aor.apply(ref["X"]), axis=0) / np.linalg.norm(Bh, axis=0)
     np.testing.assert_allclose(rel, rel_ref, rtol=1e-6, atol=1e-13)
+
+
+@pytest.mark.parametrize("kind,dims,k,P", [("Laplace3D", (12, 10, 8), 8, 2), ("Laplace3D", (12, 10, 7), 5, 3),
+                                           ("Brick3D", (10, 8, 9), 4, 3), ("Brick3D", (14, 6, 5), 8, 4)])
+def test_distributed_spmm_march_bit_exact(kind, dims, k, P):
+    """The plane march on P ranks (loopback): slabs of whole planes take it on every rank; a
+    row split in mid-plane (12 x 10 x 7 over 3 ranks, 14 x 6 x 5 over 4) puts templated pairs
+    across the local line / plane edges, so march_check declines there and that rank keeps the
+    template kernel.  Every rank bit for bit against the oracle's P-rank product."""
+    import trilinos_amd as ta
+    from oracle import epetra as oe
+    n, gen = _gen(kind, dims)
+    X, _ = oe.epetra_random_mv(43, n, k)
+    Yref = oe.DistCrs(gen, n, P).apply(X)
+    plane = dims[0] * dims[1]
+
+    def rank_fn(comm):
+        first, nloc = ta.uniform_map(n, comm.nranks, comm.rank)
+        A = ta.CrsMatrix.galeri(comm, kind, *dims)
+        Xd = ta.MultiVector(comm, n, k)
+        Xd.upload(X[first:first + nloc])
+        Yd = ta.MultiVector(comm, n, k)
+        A.apply(Xd, Yd)
+        return first, Yd.download(), A.spmm_kernel(), first % plane == 0 and nloc % plane == 0
+
+    res = run_ranks(P, rank_fn)
+    Y = np.zeros((n, k))
+    for first, y, kern, aligned in res:
+        Y[first:first + y.shape[0]] = y
+        if aligned:
+            assert kern == "march"
+    assert np.array_equal(Y, Yref)

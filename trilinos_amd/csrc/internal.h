@@ -111,6 +111,24 @@ void launch_spmm_tpl(hipStream_t s, int n_local, const unsigned char *tid, const
 bool launch_spmm_tpl3(hipStream_t s, int n_local, const unsigned char *tid, const unsigned long long *grp, int ntpl,
                       int G, const int *centers, const double *vals, int nvals, MvDesc X, MvDesc Y, double alpha,
                       double beta, const double *colscale = nullptr, int xcd_slabs = 0, int kcmax = 8);
+// The 2.5-D march over the same stencil-group templates (make_march_geometry, plan.cpp): the
+// local pairs read as planes of nyl lines of nxp pairs, group g's centre = ga[g] planes +
+// gb[g] lines.  Workgroups own 64-pair x 4-line tiles and march a slab of planes, staging each
+// plane tile (with a one-pair / one-line halo) in LDS once, so every X pair is loaded from
+// memory about once instead of once per key.  Pairs whose keys would cross a line or plane
+// edge of this geometry must not be templated (march_check counts them; the runtime uses the
+// march only when there are none).  Same products and stored-order sums: same bits.
+struct MarchGeom {
+  int nxp = 0, nyl = 0, plane = 0, nz = 0;  // pairs per line, lines per plane, pairs per plane, planes
+  int ga[9] = {}, gb[9] = {};
+};
+bool launch_spmm_march(hipStream_t s, int n_local, const unsigned char *tid, const unsigned long long *grp, int ntpl,
+                       int G, const MarchGeom &geom, const double *vals, int nvals, MvDesc X, MvDesc Y, double alpha,
+                       double beta, const double *colscale = nullptr, int kcmax = 2, int sz = 0);
+// Number of templated pairs that the march geometry cannot serve (a used x-neighbour half
+// across a line end, a group line outside the plane).  tbounds: per template {needs x-1 half,
+// needs x+1 half, lowest group line offset, highest}.
+int march_check(hipStream_t s, int npairs, const unsigned char *tid, const int4 *tbounds, int ntpl, int nxp, int nyl);
 // out[r] = omega * a[r] (r < n)
 void launch_scaled_copy(hipStream_t s, const double *a, double omega, double *out, int n);
 

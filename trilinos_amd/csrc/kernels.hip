@@ -1034,6 +1034,280 @@ bool launch_spmm_tpl3(hipStream_t s, int n_local, const unsigned char *tid, cons
   return true;
 }
 
+// -------------------------------------------------------------------------------------
+// SpMM x k over the stencil-group templates as a 2.5-D march (geometry: make_march_geometry,
+// plan.cpp).  The template kernels gather every key of every pair from memory -- 7 (9 with
+// lane sharing) 16-byte loads per pair and column, each X pair fetched once per pair that
+// reads it; the 7-point launch kept the texture data path 96 % busy
+// (profiles/r2e_spmm_cache_pmc.json).  Here a workgroup owns a tile of 64 pairs x 4 lines and
+// walks a slab of planes: each plane tile, with a one-pair and one-line halo, is loaded once
+// into a 4-plane LDS ring (planes z - 1, z, z + 1 read, z + 2 being written: one barrier per
+// plane), the next plane's loads are in flight while the current one is computed, and every
+// key of a pair is then an LDS read -- the group centre (x, y + b, z + a), the left
+// neighbour's high half and the right neighbour's low half.  Products, their order and the
+// zero-for-unused rule are k_spmm_tpl3's (its per-group sums in stored column order, no FMA),
+// so the result is the same bits.  With cs the staged operand is (omega d^-1) x, formed once
+// per X pair as k_jacobi forms it.  Tiles are dealt to the XCDs in contiguous ranges of
+// consecutive lines (workgroup b runs on XCD b mod 8), so the line halo a tile loads was
+// usually just loaded by its neighbour on the same XCD.
+// -------------------------------------------------------------------------------------
+constexpr int kMarchTX = 64, kMarchTY = 4;
+constexpr int kMarchLX = kMarchTX + 2, kMarchLY = kMarchTY + 2, kMarchPl = kMarchLX * kMarchLY;
+
+__device__ __forceinline__ void march_barrier() {  // LDS hand-off only: keeps global loads in flight
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int KC, int G>
+__global__ __launch_bounds__(256) void k_spmm_march(int npairs, int n_local, const unsigned char *__restrict__ tid,
+                                                    const unsigned long long *__restrict__ grp, int ngrp,
+                                                    MarchGeom mg, int txn, int tyn, int tzn, int sz,
+                                                    const double *__restrict__ vals, int nvals, MvDesc X, MvDesc Y,
+                                                    double alpha, double beta, const double *__restrict__ cs) {
+#pragma clang fp contract(off)
+  extern __shared__ __attribute__((aligned(16))) double march_lds[];
+  d2 *ring = (d2 *)march_lds;                                  // [4][KC][kMarchLY][kMarchLX]
+  double *s_val = march_lds + 2 * 4 * KC * kMarchPl;           // 256 dictionary slots
+  unsigned long long *s_grp = (unsigned long long *)(s_val + 256);
+  __shared__ int s_gz[G], s_gl[G];  // group g: plane offset, line offset x kMarchLX
+  const int t = threadIdx.x;
+  s_val[t] = t < nvals ? vals[t] : 0.0;
+  for (int i = t; i < ngrp; i += 256) s_grp[i] = grp[i];
+  if (t < G) {
+    s_gz[t] = mg.ga[t];
+    s_gl[t] = mg.gb[t] * kMarchLX;
+  }
+  // tile of this workgroup: XCD b mod 8 takes the b-th eighth of the tiles, lines fastest
+  const int ntile = txn * tyn * tzn, per = (ntile + 7) >> 3;
+  const int tile = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+  if (tile >= ntile) return;  // uniform: the whole workgroup leaves before any barrier
+  const int ty = tile % tyn, tx = (tile / tyn) % txn, tz = tile / (tyn * txn);
+  const int lx = t & 63, ly = t >> 6;
+  // load slot 0: this thread's own pair; slot 1 (t < 140): a halo pair (two halo lines of 64,
+  // then the left / right halo pair of each of the 6 tile lines)
+  int sx[2], sy[2], spos[2];
+  sx[0] = tx * kMarchTX + lx;
+  sy[0] = ty * kMarchTY + ly;
+  spos[0] = (ly + 1) * kMarchLX + lx + 1;
+  {
+    int line, xp;
+    if (t < 128) {
+      line = t < 64 ? 0 : kMarchLY - 1;
+      xp = lx + 1;
+    } else {
+      const int e = t - 128;
+      line = e >> 1;
+      xp = (e & 1) ? kMarchLX - 1 : 0;
+    }
+    sx[1] = tx * kMarchTX + xp - 1;
+    sy[1] = ty * kMarchTY + line - 1;
+    spos[1] = line * kMarchLX + xp;
+  }
+  bool sok[2];
+  int soff[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    sok[h] = (h == 0 || t < 140) && sx[h] >= 0 && sx[h] < mg.nxp && sy[h] >= 0 && sy[h] < mg.nyl;
+    soff[h] = sok[h] ? sy[h] * mg.nxp + sx[h] : 0;
+  }
+  const bool own = sok[0];
+  const int z0 = tz * sz, z1 = min(z0 + sz, mg.nz);
+  const int k = Y.ncols;
+  __syncthreads();  // dictionary and groups
+
+  for (int c0 = 0; c0 < k; c0 += KC) {
+    const int kc = min(KC, k - c0);
+    const double *xc[KC];
+    double *yc[KC];
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+      xc[c] = colp(X, c0 + (c < kc ? c : 0));
+      yc[c] = colp(Y, c0 + (c < kc ? c : 0));
+    }
+    d2 v[2][KC];
+    d2 sc[2];
+    int tnext = 0xFF;
+    // loads of plane q into v / sc (zeros outside the local pairs), and q's template ids
+    auto load = [&](int q) __attribute__((always_inline)) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const long long pr = (long long)q * mg.plane + soff[h];
+        const bool ok = sok[h] && q >= 0 && q < mg.nz && pr < npairs;
+        const long long pc = ok ? pr : 0;
+#pragma unroll
+        for (int c = 0; c < KC; ++c) v[h][c] = (ok && c < kc) ? *(const d2 *)(xc[c] + 2 * pc) : d2{0.0, 0.0};
+        if (cs) sc[h] = ok ? *(const d2 *)(cs + 2 * pc) : d2{0.0, 0.0};
+      }
+      {
+        const long long pr = (long long)q * mg.plane + soff[0];
+        tnext = (own && q >= 0 && q < mg.nz && pr < npairs) ? (int)tid[pr] : 0xFF;
+      }
+    };
+    auto stage = [&](int q) __attribute__((always_inline)) {  // v -> ring slot of plane q
+      d2 *r = ring + (size_t)(q & 3) * KC * kMarchPl;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (h == 1 && t >= 140) break;
+#pragma unroll
+        for (int c = 0; c < KC; ++c) r[c * kMarchPl + spos[h]] = cs ? sc[h] * v[h][c] : v[h][c];
+      }
+    };
+    if (c0 > 0) march_barrier();  // the previous chunk's last plane has been read
+    load(z0 - 1);
+    stage(z0 - 1);
+    load(z0);
+    stage(z0);
+    int tcur = tnext;
+    load(z0 + 1);
+    for (int z = z0; z < z1; ++z) {
+      stage(z + 1);
+      const int tz_ = tcur;
+      tcur = tnext;
+      load(z + 2);  // in flight through this plane's products
+      march_barrier();
+      const long long p = (long long)z * mg.plane + soff[0];
+      if (own && tz_ != 0xFF) {
+        double sa[KC], sb[KC];
+#pragma unroll
+        for (int c = 0; c < KC; ++c) sa[c] = sb[c] = 0.0;
+        // not unrolled: unrolled, all groups' operands and coefficients are hoisted (256 VGPRs)
+#pragma unroll 1
+        for (int g = 0; g < G; ++g) {
+          const unsigned long long sl = s_grp[tz_ * G + g];
+          const unsigned s0 = sl & 0xFF, s1 = (sl >> 8) & 0xFF, s2 = (sl >> 16) & 0xFF;
+          const unsigned s3 = (sl >> 24) & 0xFF, s4 = (sl >> 32) & 0xFF, s5 = (sl >> 40) & 0xFF;
+          const double w0 = s_val[s0], w1 = s_val[s1], w2 = s_val[s2];
+          const double w3 = s_val[s3], w4 = s_val[s4], w5 = s_val[s5];
+          const d2 *b = ring + ((z + s_gz[g]) & 3) * (KC * kMarchPl) + s_gl[g] + (ly + 1) * kMarchLX + lx + 1;
+#pragma unroll
+          for (int c = 0; c < KC; ++c) {
+            const d2 x = b[c * kMarchPl];
+            const double left = b[c * kMarchPl - 1].y;   // row 0's x - 1
+            const double right = b[c * kMarchPl + 1].x;  // row 1's x + 1
+            const double pa0 = w0 * left, pa1 = w1 * x.x, pa2 = w2 * x.y;
+            const double pb0 = w3 * x.x, pb1 = w4 * x.y, pb2 = w5 * right;
+            sa[c] = sa[c] + (s0 != 0xFF ? pa0 : 0.0);
+            sa[c] = sa[c] + (s1 != 0xFF ? pa1 : 0.0);
+            sa[c] = sa[c] + (s2 != 0xFF ? pa2 : 0.0);
+            sb[c] = sb[c] + (s3 != 0xFF ? pb0 : 0.0);
+            sb[c] = sb[c] + (s4 != 0xFF ? pb1 : 0.0);
+            sb[c] = sb[c] + (s5 != 0xFF ? pb2 : 0.0);
+          }
+        }
+        const long long ra = 2 * p;
+        const bool hasb = ra + 1 < n_local;
+#pragma unroll
+        for (int c = 0; c < KC; ++c) {
+          if (c >= kc) break;
+          double *yp = yc[c] + ra;
+          double a = sa[c], bb = sb[c];
+          if (beta == 0.0) {
+            if (alpha != 1.0) {
+              a = alpha * a;
+              bb = alpha * bb;
+            }
+          } else {
+            a = alpha * a + beta * yp[0];
+            if (hasb) bb = alpha * bb + beta * yp[1];
+          }
+          if (hasb)
+            *(d2 *)yp = d2{a, bb};
+          else
+            yp[0] = a;
+        }
+      }
+    }
+  }
+}
+
+template <int KC, int G>
+static void march_cols(hipStream_t s, int npairs, int n_local, const unsigned char *tid,
+                       const unsigned long long *grp, int ngrp, const MarchGeom &g, int sz, const double *vals,
+                       int nvals, MvDesc X, MvDesc Y, double alpha, double beta, const double *cs) {
+  const int txn = cdiv(g.nxp, kMarchTX), tyn = cdiv(g.nyl, kMarchTY), tzn = cdiv(g.nz, sz);
+  const int ntile = txn * tyn * tzn;
+  const size_t lds = sizeof(d2) * 4 * KC * kMarchPl + sizeof(double) * 256 + sizeof(unsigned long long) * ngrp;
+  k_spmm_march<KC, G><<<8 * ((ntile + 7) / 8), 256, lds, s>>>(npairs, n_local, tid, grp, ngrp, g, txn, tyn, tzn, sz,
+                                                               vals, nvals, X, Y, alpha, beta, cs);
+}
+
+bool launch_spmm_march(hipStream_t s, int n_local, const unsigned char *tid, const unsigned long long *grp, int ntpl,
+                       int G, const MarchGeom &geom, const double *vals, int nvals, MvDesc X, MvDesc Y, double alpha,
+                       double beta, const double *colscale, int kcmax, int sz) {
+  const int npairs = (n_local + 1) / 2;
+  if (npairs <= 0 || Y.ncols <= 0) return true;
+  if (G != 9 && G != 5 && G != 3) return false;
+  if (geom.nxp <= 0 || geom.nyl <= 0 || geom.plane != geom.nxp * geom.nyl ||
+      (long long)geom.nz * geom.plane < npairs)
+    return false;
+  const int ngrp = ntpl * G;
+  if (sz <= 0) {
+    // z slabs: about one resident round of workgroups, at least 8 planes per slab
+    static int cus = 0;
+    if (!cus) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        cus = 256;
+    }
+    const int per_cu = kcmax >= 2 ? 3 : 6;
+    const long long cols = (long long)cdiv(geom.nxp, kMarchTX) * cdiv(geom.nyl, kMarchTY);
+    const long long slabs = std::max(1LL, std::min((long long)cus * per_cu / cols, (long long)cdiv(geom.nz, 8)));
+    sz = cdiv(geom.nz, slabs);
+  }
+#define MARCH(KC)                                                                                                 \
+  if (G == 9)                                                                                                     \
+    march_cols<KC, 9>(s, npairs, n_local, tid, grp, ngrp, geom, sz, vals, nvals, X, Y, alpha, beta, colscale);     \
+  else if (G == 5)                                                                                                \
+    march_cols<KC, 5>(s, npairs, n_local, tid, grp, ngrp, geom, sz, vals, nvals, X, Y, alpha, beta, colscale);     \
+  else                                                                                                            \
+    march_cols<KC, 3>(s, npairs, n_local, tid, grp, ngrp, geom, sz, vals, nvals, X, Y, alpha, beta, colscale);
+  if (kcmax >= 2 && Y.ncols >= 2) {
+    MARCH(2)
+  } else {
+    MARCH(1)
+  }
+#undef MARCH
+  LAUNCH_CHECK();
+  return true;
+}
+
+__global__ __launch_bounds__(256) void k_march_check(int npairs, const unsigned char *__restrict__ tid,
+                                                     const int4 *__restrict__ tb, int nxp, int nyl,
+                                                     int *__restrict__ bad) {
+  int n = 0;
+  for (int p = blockIdx.x * 256 + threadIdx.x; p < npairs; p += gridDim.x * 256) {
+    const int t = tid[p];
+    if (t == 0xFF) continue;
+    const int x = p % nxp, y = (p / nxp) % nyl;
+    const int4 b = tb[t];
+    n += (b.x && x == 0) || (b.y && x == nxp - 1) || y + b.z < 0 || y + b.w >= nyl;
+  }
+  for (int off = 32; off > 0; off >>= 1) n += __shfl_down(n, off, 64);
+  if ((threadIdx.x & 63) == 0 && n) atomicAdd(bad, n);
+}
+
+int march_check(hipStream_t s, int npairs, const unsigned char *tid, const int4 *tbounds, int ntpl, int nxp,
+                int nyl) {
+  if (npairs <= 0) return 0;
+  int *d = nullptr;
+  int4 *dtb = nullptr;
+  MIG_HIP(hipMalloc(&d, sizeof(int)));
+  MIG_HIP(hipMalloc(&dtb, sizeof(int4) * ntpl));
+  MIG_HIP(hipMemcpyAsync(dtb, tbounds, sizeof(int4) * ntpl, hipMemcpyHostToDevice, s));
+  MIG_HIP(hipMemsetAsync(d, 0, sizeof(int), s));
+  k_march_check<<<std::min(cdiv(npairs, 256), 4096), 256, 0, s>>>(npairs, tid, dtb, nxp, nyl, d);
+  LAUNCH_CHECK();
+  int h = 0;
+  MIG_HIP(hipMemcpyAsync(&h, d, sizeof(int), hipMemcpyDeviceToHost, s));
+  MIG_HIP(hipStreamSynchronize(s));
+  hipFree(d);
+  hipFree(dtb);
+  return h;
+}
+
 void launch_spmm_tpl(hipStream_t s, int n_local, const unsigned char *tid, const int2 *rec, int ntpl, int maxk,
                      const double *vals, int nvals, MvDesc X, MvDesc Y, double alpha, double beta,
                      const double *colscale, int xcd_slabs, int kcmax) {

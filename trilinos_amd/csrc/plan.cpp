@@ -617,4 +617,64 @@ bool make_stencil_groups(const PairTemplates &pt, StencilGroups &out) {
   return true;
 }
 
+bool make_march_geometry(const StencilGroups &sg, int ntpl, int npairs, MarchGeometry &out) {
+  out = MarchGeometry();
+  const int G = sg.G;
+  if (G < 1 || npairs <= 0) return false;
+  std::vector<int> pos;
+  for (int c : sg.center)
+    if (c > 0) pos.push_back(c);
+  std::sort(pos.begin(), pos.end());
+  if (pos.empty()) return false;
+  const int nxp = pos[0];
+  std::vector<long long> cand;
+  for (int c : pos)
+    if (c > nxp) {
+      cand.push_back(c);
+      cand.push_back((long long)c + nxp);
+    }
+  for (long long P : cand) {
+    if (P % nxp != 0 || P / nxp < 2 || P > (1LL << 30)) continue;
+    std::vector<int> ga(G), gb(G);
+    bool all = true, deep = false;
+    for (int g = 0; g < G && all; ++g) {
+      bool found = false;
+      for (int a : {0, -1, 1})
+        for (int b : {0, -1, 1})
+          if (!found && (long long)a * P + (long long)b * nxp == sg.center[(size_t)g]) {
+            ga[(size_t)g] = a;
+            gb[(size_t)g] = b;
+            found = true;
+          }
+      all = found;
+      deep = deep || (found && ga[(size_t)g] != 0);
+    }
+    if (!all || !deep) continue;
+    out.nxp = nxp;
+    out.plane = (int)P;
+    out.nyl = (int)(P / nxp);
+    out.nz = (int)((npairs + P - 1) / P);
+    out.ga = ga;
+    out.gb = gb;
+    out.tb.assign((size_t)4 * ntpl, 0);
+    for (int t = 0; t < ntpl; ++t) {
+      int *b = &out.tb[(size_t)4 * t];
+      bool any = false;
+      for (int g = 0; g < G; ++g) {
+        const unsigned long long w = sg.slots[(size_t)t * G + g];
+        bool used = false;
+        for (int byte = 0; byte < 6; ++byte) used = used || ((w >> (8 * byte)) & 0xFF) != kTplUnused;
+        if (!used) continue;
+        if ((w & 0xFF) != kTplUnused) b[0] = 1;
+        if (((w >> 40) & 0xFF) != kTplUnused) b[1] = 1;
+        b[2] = any ? std::min(b[2], gb[(size_t)g]) : gb[(size_t)g];
+        b[3] = any ? std::max(b[3], gb[(size_t)g]) : gb[(size_t)g];
+        any = true;
+      }
+    }
+    return true;
+  }
+  return false;
+}
+
 }  // namespace migmres

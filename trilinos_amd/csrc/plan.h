@@ -136,6 +136,20 @@ struct StencilGroups {
 };
 bool make_stencil_groups(const PairTemplates &pt, StencilGroups &out);
 
+// Geometry of the stencil groups for the 2.5-D march (k_spmm_march, kernels.hip): pair
+// offsets nxp (one grid line) and plane = nxp * nyl (one grid plane) such that every group
+// centre is ga * plane + gb * nxp with ga, gb in {-1, 0, 1} and some ga != 0 (a 3-D stencil);
+// nz = planes covering npairs.  nxp is the smallest positive centre, plane the first
+// candidate (a positive centre, or one plus nxp) that decomposes every centre.  tb holds per
+// template {uses a left-neighbour half, uses a right-neighbour half, lowest gb, highest gb}
+// of its used groups, for the device check that no templated pair's keys leave its line or
+// plane under this geometry (march_check).  Returns false when no such geometry exists.
+struct MarchGeometry {
+  int nxp = 0, nyl = 0, plane = 0, nz = 0;
+  std::vector<int> ga, gb, tb;
+};
+bool make_march_geometry(const StencilGroups &sg, int ntpl, int npairs, MarchGeometry &out);
+
 void galeri_rows(const std::string &kind, int nx, int ny, int nz, long long first, int n_local,
                  std::vector<long long> &rowptr, std::vector<long long> &gcols,
                  std::vector<double> &vals);

@@ -807,13 +807,37 @@ static void setup_template_kernels(migmres_crs *A, const PairTemplates &pt) {
   // x-neighbour triples (k_spmm_tpl3); MIGMRES_NO_TPL3=1 keeps k_spmm_tpl
   const bool short_ok = env_on("MIGMRES_TPL3_SHORT");  // 7-point templates too (tuning)
   StencilGroups sg;
-  if (!env_on("MIGMRES_NO_TPL3") && (pt.maxk > 12 || short_ok) && make_stencil_groups(pt, sg) &&
-      (sg.G == 9 || sg.G == 5 || sg.G == 3)) {
+  const bool groups = make_stencil_groups(pt, sg) && (sg.G == 9 || sg.G == 5 || sg.G == 3);
+  auto upload_groups = [&] {
     MIG_HIP(hipMalloc(&A->d_tpl3_grp, sizeof(unsigned long long) * sg.slots.size()));
     MIG_HIP(hipMemcpy(A->d_tpl3_grp, sg.slots.data(), sizeof(unsigned long long) * sg.slots.size(),
                       hipMemcpyHostToDevice));
     A->tpl3_center = sg.center;
     A->tpl3_G = sg.G;
+  };
+  // the plane march (k_spmm_march) for 3-D stencil groups; MIGMRES_NO_MARCH=1 keeps the
+  // template kernels
+  MarchGeometry mg;
+  if (!env_on("MIGMRES_NO_MARCH") && groups && make_march_geometry(sg, pt.ntpl, pt.npairs, mg) &&
+      march_check(A->ctx->stream, pt.npairs, A->d_tpl_id, (const int4 *)mg.tb.data(), pt.ntpl, mg.nxp, mg.nyl) == 0) {
+    upload_groups();
+    A->march.nxp = mg.nxp;
+    A->march.nyl = mg.nyl;
+    A->march.plane = mg.plane;
+    A->march.nz = mg.nz;
+    for (int g = 0; g < sg.G; ++g) {
+      A->march.ga[g] = mg.ga[(size_t)g];
+      A->march.gb[g] = mg.gb[(size_t)g];
+    }
+    A->use_march = true;
+    const char *kc = std::getenv("MIGMRES_MARCH_KC");
+    A->march_kc = kc ? std::atoi(kc) : 2;
+    const char *sz = std::getenv("MIGMRES_MARCH_SZ");
+    A->march_sz = sz ? std::atoi(sz) : 0;
+    return;
+  }
+  if (!env_on("MIGMRES_NO_TPL3") && (pt.maxk > 12 || short_ok) && groups) {
+    upload_groups();
     A->use_tpl3 = true;
     const char *sl = std::getenv("MIGMRES_TPL3_SLABS");
     A->tpl3_slabs = sl ? std::atoi(sl) : 1;
@@ -1187,9 +1211,14 @@ static void crs_apply_impl(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, d
   if (A.use_tpl) {
     // templated pairs read no ghost column: they run while the halo is in flight, then the
     // pairs that do read one go to the fallback kernel
-    if (!A.use_tpl3 || !launch_spmm_tpl3(c->stream, A.n_local, A.d_tpl_id, A.d_tpl3_grp, A.tpl_ntpl, A.tpl3_G,
-                                         A.tpl3_center.data(), A.d_tpl_val, A.tpl_nvals, X.desc(), Y.desc(),
-                                         alpha, beta, cs.own, A.tpl3_slabs, A.tpl3_kc))
+    bool done = A.use_march && launch_spmm_march(c->stream, A.n_local, A.d_tpl_id, A.d_tpl3_grp, A.tpl_ntpl,
+                                                 A.tpl3_G, A.march, A.d_tpl_val, A.tpl_nvals, X.desc(), Y.desc(),
+                                                 alpha, beta, cs.own, A.march_kc, A.march_sz);
+    done = done || (A.use_tpl3 && launch_spmm_tpl3(c->stream, A.n_local, A.d_tpl_id, A.d_tpl3_grp, A.tpl_ntpl,
+                                                   A.tpl3_G, A.tpl3_center.data(), A.d_tpl_val, A.tpl_nvals,
+                                                   X.desc(), Y.desc(), alpha, beta, cs.own, A.tpl3_slabs,
+                                                   A.tpl3_kc));
+    if (!done)
       launch_spmm_tpl(c->stream, A.n_local, A.d_tpl_id, A.d_tpl_rec, A.tpl_ntpl, A.tpl_maxk, A.d_tpl_val,
                       A.tpl_nvals, X.desc(), Y.desc(), alpha, beta, cs.own, A.tpl_slabs, A.tpl_kc);
     if (halo) MIG_HIP(hipStreamWaitEvent(c->stream, c->ev_halo, 0));
@@ -1271,6 +1300,7 @@ extern "C" int migmres_crs_spmm_kernel(const migmres_crs *A, int *kind) {
   return guard([&] {
     MIG_CHECK(A && kind, "bad arguments");
     *kind = A->use_bsr3 ? MIGMRES_SPMM_BSR3
+            : A->use_march ? MIGMRES_SPMM_MARCH
             : A->use_tpl3 ? MIGMRES_SPMM_TPL3
             : A->use_tpl ? MIGMRES_SPMM_TPL
             : A->use_pairs ? MIGMRES_SPMM_PAIR
@@ -1302,7 +1332,7 @@ extern "C" int migmres_crs_format_digest(const migmres_crs *A, unsigned long lon
     const int nl = A->n_local, P = (nl + 1) / 2;
     d.push_back((unsigned long long)A->use_pairs | (unsigned long long)A->use_sell << 1 |
                 (unsigned long long)A->use_bsr3 << 2 | (unsigned long long)A->use_tpl << 3 |
-                (unsigned long long)A->use_tpl3 << 4);
+                (unsigned long long)A->use_tpl3 << 4 | (unsigned long long)A->use_march << 5);
     num(A->spmm_fixed_bytes);
     if (A->use_pairs) {
       const size_t nch = (size_t)(P + 63) / 64;
@@ -1339,7 +1369,10 @@ extern "C" int migmres_crs_format_digest(const migmres_crs *A, unsigned long lon
       d.push_back(fnv_bytes(A->d_tpl_val, sizeof(double) * A->tpl_nvals));
       d.push_back(fnv_bytes(A->d_tpl_rest, sizeof(int) * A->n_tpl_rest));
     }
-    if (A->use_tpl3) d.push_back(fnv_bytes(A->d_tpl3_grp, sizeof(unsigned long long) * A->tpl_ntpl * A->tpl3_G));
+    if (A->use_tpl3 || A->use_march)
+      d.push_back(fnv_bytes(A->d_tpl3_grp, sizeof(unsigned long long) * A->tpl_ntpl * A->tpl3_G));
+    if (A->use_march)
+      d.push_back((unsigned long long)A->march.nxp << 32 | (unsigned)A->march.plane);
     d.push_back((unsigned long long)A->n_sel_int << 32 | (unsigned)A->n_sel_bnd);
     d.push_back(fnv_bytes(A->d_sel_int, sizeof(int) * A->n_sel_int));
     d.push_back(fnv_bytes(A->d_sel_bnd, sizeof(int) * A->n_sel_bnd));

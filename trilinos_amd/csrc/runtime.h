@@ -173,6 +173,11 @@ struct migmres_crs {
   int tpl3_G = 0;
   bool use_tpl3 = false;
   int tpl3_slabs = 0, tpl3_kc = 8;  // walk order (XCD slabs) and columns per launch (tuning)
+  // the same groups as a 2.5-D plane march (k_spmm_march) when they have a 3-D grid geometry
+  // that every templated pair fits (make_march_geometry + march_check)
+  migmres::MarchGeom march;
+  bool use_march = false;
+  int march_kc = 2, march_sz = 0;  // columns staged per plane, planes per slab (0: auto)
   int tpl_slabs = 0, tpl_kc = 8;
   int n_tpl_rest = 0;
   double spmm_fixed_bytes = 0.0;  // matrix-format bytes one apply reads (bench accounting)

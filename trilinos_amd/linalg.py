@@ -176,11 +176,11 @@ class CrsMatrix:
         return cls(comm, ng.value, _handle=h)
 
     def spmm_kernel(self):
-        """The SpMM kernel apply() runs: "csr", "pair", "sell", "tpl", "tpl3" or "bsr3"
+        """The SpMM kernel apply() runs: "csr", "pair", "sell", "tpl", "tpl3", "bsr3" or "march"
         (migmres_crs_spmm_kernel)."""
         v = C.c_int()
         call("migmres_crs_spmm_kernel", self.h, C.byref(v))
-        return ("csr", "pair", "sell", "tpl", "tpl3", "bsr3")[v.value]
+        return ("csr", "pair", "sell", "tpl", "tpl3", "bsr3", "march")[v.value]
 
     def format_digest(self):
         """64-bit digests of the SpMM format plans this operator holds
