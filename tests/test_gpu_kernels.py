@@ -404,21 +404,25 @@ def test_spmm_bsr3_detects_not_assumes(comm):
 
 @pytest.mark.parametrize("kind,dims,k", [("Laplace3D", (12, 11, 10), 8), ("Laplace3D", (16, 9, 7), 1),
                                          ("Laplace3D", (130, 6, 5), 3), ("Laplace3D", (8, 7, 9), 9),
-                                         ("Laplace3D", (4, 3, 3), 2), ("Brick3D", (12, 11, 10), 8),
+                                         ("Laplace3D", (6, 3, 3), 2), ("Brick3D", (12, 11, 10), 8),
                                          ("Brick3D", (20, 6, 5), 16), ("Brick3D", (134, 5, 4), 5),
                                          ("Brick3D", (6, 5, 4), 2), ("Brick3D", (10, 10, 10), 3)])
 @pytest.mark.parametrize("alpha,beta", [(1.0, 0.0), (-1.0, 1.0), (0.5, -2.0)])
-def test_spmm_march_bit_exact(comm, kind, dims, k, alpha, beta):
-    """7- and 27-point operators on even-nx grids take the 2.5-D plane march (plane tiles of
-    64 pairs x 4 lines staged once in LDS; partial x tiles at nx = 130 / 134, partial line
-    tiles, a few planes, odd column counts): bit for bit against the oracle, and
-    Y = alpha A X + beta Y."""
+@pytest.mark.parametrize("generic", [False, True])
+def test_spmm_march_bit_exact(comm, kind, dims, k, alpha, beta, generic, monkeypatch):
+    """The 2.5-D plane march (plane tiles of 64 pairs x 4 lines staged in LDS; partial x tiles
+    at nx = 130 / 134, partial line tiles, a few planes, odd column counts): by default the
+    7-point specialisation for Laplace3D (the 27-point operator keeps the lane-shared template
+    kernel), with MIGMRES_MARCH_GENERIC=1 the general form for both -- bit for bit against
+    the oracle, and Y = alpha A X + beta Y."""
     import trilinos_amd as ta
     from oracle import epetra as oe
+    if generic:
+        monkeypatch.setenv("MIGMRES_MARCH_GENERIC", "1")
     nx, ny, nz = dims
     n = nx * ny * nz
     A = ta.CrsMatrix.galeri(comm, kind, nx, ny, nz)
-    assert A.spmm_kernel() == "march"
+    assert A.spmm_kernel() == ("march" if generic or kind == "Laplace3D" else "tpl3")
     gen = (lambda f, m: oe.brick3d_rows(nx, ny, nz, f, m)) if kind == "Brick3D" else \
         (lambda f, m: oe.laplace3d_rows(nx, ny, nz, f, m))
     Aor = oe.DistCrs(gen, n, 1)
@@ -430,16 +434,22 @@ def test_spmm_march_bit_exact(comm, kind, dims, k, alpha, beta):
     assert np.array_equal(Yd.download(), want)
 
 
-@pytest.mark.parametrize("kc,sz", [("1", "1"), ("1", "3"), ("2", "2"), ("2", "5"), ("2", "64")])
-@pytest.mark.parametrize("kind", ["Laplace3D", "Brick3D"])
-def test_spmm_march_slabs_bit_exact(comm, kind, kc, sz, monkeypatch):
-    """The march's slab and column-chunk knobs (MIGMRES_MARCH_SZ planes per workgroup -- one
-    plane, ragged last slabs, one slab for all -- and MIGMRES_MARCH_KC columns per staged plane)
-    change only the walk: same bits as the oracle."""
+@pytest.mark.parametrize("kind,generic,kc,sz,pd", [("Laplace3D", False, "1", "1", "1"), ("Laplace3D", False, "1", "3", "2"),
+                                                   ("Laplace3D", False, "1", "5", "3"), ("Laplace3D", False, "1", "64", "4"),
+                                                   ("Laplace3D", False, "1", "2", "4"), ("Laplace3D", True, "1", "1", "1"),
+                                                   ("Laplace3D", True, "2", "5", "2"), ("Brick3D", True, "1", "3", "2"),
+                                                   ("Brick3D", True, "2", "2", "1"), ("Brick3D", True, "2", "64", "2")])
+def test_spmm_march_slabs_bit_exact(comm, kind, generic, kc, sz, pd, monkeypatch):
+    """The march's walk knobs -- MIGMRES_MARCH_SZ planes per workgroup (one plane, ragged last
+    slabs, one slab for all), MIGMRES_MARCH_PD planes of loads in flight, MIGMRES_MARCH_KC
+    columns per staged plane (general form) -- change only the walk: same bits as the oracle."""
     import trilinos_amd as ta
     from oracle import epetra as oe
+    if generic:
+        monkeypatch.setenv("MIGMRES_MARCH_GENERIC", "1")
     monkeypatch.setenv("MIGMRES_MARCH_KC", kc)
     monkeypatch.setenv("MIGMRES_MARCH_SZ", sz)
+    monkeypatch.setenv("MIGMRES_MARCH_PD", pd)
     nx, ny, nz, k = 14, 9, 11, 5
     n = nx * ny * nz
     A = ta.CrsMatrix.galeri(comm, kind, nx, ny, nz)
@@ -450,4 +460,3 @@ def test_spmm_march_slabs_bit_exact(comm, kind, kc, sz, monkeypatch):
     Yd = ta.MultiVector(comm, n, k)
     A.apply(_upload(ta, comm, X), Yd)
     assert np.array_equal(Yd.download(), oe.DistCrs(gen, n, 1).apply(X))
-

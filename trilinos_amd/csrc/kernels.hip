@@ -1060,7 +1060,7 @@ __device__ __forceinline__ void march_barrier() {  // LDS hand-off only: keeps g
   asm volatile("" ::: "memory");
 }
 
-template <int KC, int G>
+template <int KC, int G, int PD>
 __global__ __launch_bounds__(256) void k_spmm_march(int npairs, int n_local, const unsigned char *__restrict__ tid,
                                                     const unsigned long long *__restrict__ grp, int ngrp,
                                                     MarchGeom mg, int txn, int tyn, int tzn, int sz,
@@ -1126,47 +1126,7 @@ __global__ __launch_bounds__(256) void k_spmm_march(int npairs, int n_local, con
       xc[c] = colp(X, c0 + (c < kc ? c : 0));
       yc[c] = colp(Y, c0 + (c < kc ? c : 0));
     }
-    d2 v[2][KC];
-    d2 sc[2];
-    int tnext = 0xFF;
-    // loads of plane q into v / sc (zeros outside the local pairs), and q's template ids
-    auto load = [&](int q) __attribute__((always_inline)) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const long long pr = (long long)q * mg.plane + soff[h];
-        const bool ok = sok[h] && q >= 0 && q < mg.nz && pr < npairs;
-        const long long pc = ok ? pr : 0;
-#pragma unroll
-        for (int c = 0; c < KC; ++c) v[h][c] = (ok && c < kc) ? *(const d2 *)(xc[c] + 2 * pc) : d2{0.0, 0.0};
-        if (cs) sc[h] = ok ? *(const d2 *)(cs + 2 * pc) : d2{0.0, 0.0};
-      }
-      {
-        const long long pr = (long long)q * mg.plane + soff[0];
-        tnext = (own && q >= 0 && q < mg.nz && pr < npairs) ? (int)tid[pr] : 0xFF;
-      }
-    };
-    auto stage = [&](int q) __attribute__((always_inline)) {  // v -> ring slot of plane q
-      d2 *r = ring + (size_t)(q & 3) * KC * kMarchPl;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        if (h == 1 && t >= 140) break;
-#pragma unroll
-        for (int c = 0; c < KC; ++c) r[c * kMarchPl + spos[h]] = cs ? sc[h] * v[h][c] : v[h][c];
-      }
-    };
-    if (c0 > 0) march_barrier();  // the previous chunk's last plane has been read
-    load(z0 - 1);
-    stage(z0 - 1);
-    load(z0);
-    stage(z0);
-    int tcur = tnext;
-    load(z0 + 1);
-    for (int z = z0; z < z1; ++z) {
-      stage(z + 1);
-      const int tz_ = tcur;
-      tcur = tnext;
-      load(z + 2);  // in flight through this plane's products
-      march_barrier();
+    auto products = [&](int z, int tz_) __attribute__((always_inline)) {
       const long long p = (long long)z * mg.plane + soff[0];
       if (own && tz_ != 0xFF) {
         double sa[KC], sb[KC];
@@ -1218,24 +1178,83 @@ __global__ __launch_bounds__(256) void k_spmm_march(int npairs, int n_local, con
             yp[0] = a;
         }
       }
+    };
+    // one plane's registers: both load slots' KC operands, their column scale, the own pair's
+    // template id
+    struct PlaneRegs {
+      d2 v[2][KC];
+      d2 sc[2];
+      int tid;
+    };
+    // loads of plane q (zeros outside the local pairs)
+    auto load = [&](PlaneRegs &r, int q) __attribute__((always_inline)) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const long long pr = (long long)q * mg.plane + soff[h];
+        const bool ok = sok[h] && q >= 0 && q < mg.nz && pr < npairs;
+        const long long pc = ok ? pr : 0;
+#pragma unroll
+        for (int c = 0; c < KC; ++c) r.v[h][c] = (ok && c < kc) ? *(const d2 *)(xc[c] + 2 * pc) : d2{0.0, 0.0};
+        if (cs) r.sc[h] = ok ? *(const d2 *)(cs + 2 * pc) : d2{0.0, 0.0};
+      }
+      const long long pr = (long long)q * mg.plane + soff[0];
+      r.tid = (own && q >= 0 && q < mg.nz && pr < npairs) ? (int)tid[pr] : 0xFF;
+    };
+    auto stage = [&](const PlaneRegs &r, int q) __attribute__((always_inline)) {  // -> ring slot of plane q
+      d2 *d = ring + (size_t)(q & 3) * KC * kMarchPl;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (h == 1 && t >= 140) break;
+#pragma unroll
+        for (int c = 0; c < KC; ++c) d[c * kMarchPl + spos[h]] = cs ? r.sc[h] * r.v[h][c] : r.v[h][c];
+      }
+    };
+    if (c0 > 0) march_barrier();  // the previous chunk's last plane has been read
+    PlaneRegs ra, rb;
+    load(ra, z0 - 1);
+    stage(ra, z0 - 1);
+    load(ra, z0);
+    stage(ra, z0);
+    int tcur = ra.tid;
+    load(ra, z0 + 1);
+    if (PD == 2) load(rb, z0 + 2);
+    // plane z: stage plane z + 1 from r, refill r with plane z + 1 + PD (in flight through this
+    // plane's products and, with PD = 2, the next one's), one barrier, the products
+    auto step = [&](int z, PlaneRegs &r) __attribute__((always_inline)) {
+      stage(r, z + 1);
+      const int tz_ = tcur;
+      tcur = r.tid;
+      load(r, z + 1 + PD);
+      march_barrier();
+      products(z, tz_);
+    };
+    for (int z = z0; z < z1; z += 2) {
+      step(z, ra);
+      if (z + 1 < z1) step(z + 1, PD == 2 ? rb : ra);
     }
   }
 }
 
 template <int KC, int G>
 static void march_cols(hipStream_t s, int npairs, int n_local, const unsigned char *tid,
-                       const unsigned long long *grp, int ngrp, const MarchGeom &g, int sz, const double *vals,
-                       int nvals, MvDesc X, MvDesc Y, double alpha, double beta, const double *cs) {
+                       const unsigned long long *grp, int ngrp, const MarchGeom &g, int sz, int pd,
+                       const double *vals, int nvals, MvDesc X, MvDesc Y, double alpha, double beta,
+                       const double *cs) {
   const int txn = cdiv(g.nxp, kMarchTX), tyn = cdiv(g.nyl, kMarchTY), tzn = cdiv(g.nz, sz);
   const int ntile = txn * tyn * tzn;
   const size_t lds = sizeof(d2) * 4 * KC * kMarchPl + sizeof(double) * 256 + sizeof(unsigned long long) * ngrp;
-  k_spmm_march<KC, G><<<8 * ((ntile + 7) / 8), 256, lds, s>>>(npairs, n_local, tid, grp, ngrp, g, txn, tyn, tzn, sz,
-                                                               vals, nvals, X, Y, alpha, beta, cs);
+  const int grid = 8 * ((ntile + 7) / 8);
+  if (pd == 2)
+    k_spmm_march<KC, G, 2><<<grid, 256, lds, s>>>(npairs, n_local, tid, grp, ngrp, g, txn, tyn, tzn, sz, vals, nvals,
+                                                   X, Y, alpha, beta, cs);
+  else
+    k_spmm_march<KC, G, 1><<<grid, 256, lds, s>>>(npairs, n_local, tid, grp, ngrp, g, txn, tyn, tzn, sz, vals, nvals,
+                                                   X, Y, alpha, beta, cs);
 }
 
 bool launch_spmm_march(hipStream_t s, int n_local, const unsigned char *tid, const unsigned long long *grp, int ntpl,
                        int G, const MarchGeom &geom, const double *vals, int nvals, MvDesc X, MvDesc Y, double alpha,
-                       double beta, const double *colscale, int kcmax, int sz) {
+                       double beta, const double *colscale, int kcmax, int sz, int pd) {
   const int npairs = (n_local + 1) / 2;
   if (npairs <= 0 || Y.ncols <= 0) return true;
   if (G != 9 && G != 5 && G != 3) return false;
@@ -1259,17 +1278,245 @@ bool launch_spmm_march(hipStream_t s, int n_local, const unsigned char *tid, con
   }
 #define MARCH(KC)                                                                                                 \
   if (G == 9)                                                                                                     \
-    march_cols<KC, 9>(s, npairs, n_local, tid, grp, ngrp, geom, sz, vals, nvals, X, Y, alpha, beta, colscale);     \
+    march_cols<KC, 9>(s, npairs, n_local, tid, grp, ngrp, geom, sz, pd, vals, nvals, X, Y, alpha, beta, colscale);     \
   else if (G == 5)                                                                                                \
-    march_cols<KC, 5>(s, npairs, n_local, tid, grp, ngrp, geom, sz, vals, nvals, X, Y, alpha, beta, colscale);     \
+    march_cols<KC, 5>(s, npairs, n_local, tid, grp, ngrp, geom, sz, pd, vals, nvals, X, Y, alpha, beta, colscale);     \
   else                                                                                                            \
-    march_cols<KC, 3>(s, npairs, n_local, tid, grp, ngrp, geom, sz, vals, nvals, X, Y, alpha, beta, colscale);
+    march_cols<KC, 3>(s, npairs, n_local, tid, grp, ngrp, geom, sz, pd, vals, nvals, X, Y, alpha, beta, colscale);
   if (kcmax >= 2 && Y.ncols >= 2) {
     MARCH(2)
   } else {
     MARCH(1)
   }
 #undef MARCH
+  LAUNCH_CHECK();
+  return true;
+}
+
+// -------------------------------------------------------------------------------------
+// The march for the 7-point pattern (groups (z-1), (y-1), the x line, (y+1), (z+1); only the
+// x line reads neighbour halves): measured, the general march is bound by its LDS reads --
+// per pair and column one group word, six dictionary lookups and three operand reads per group,
+// about 50 LDS instructions, more than the 7 global loads it saves.  Here:
+//  * the coefficients live in registers: a template's 30 values (5 groups x 6 slots, 0 where
+//    unused) are read from an LDS table only when a lane's template changes between planes
+//    (interior pairs keep theirs for the whole slab);
+//  * only plane z is staged (a 3-slot ring, one barrier per plane): the (z - 1) and (z + 1)
+//    centres are the lane's own pair, kept in registers from its loads, so a pair and column
+//    costs 4 LDS reads (the y - 1 and y + 1 centres, the left and right halves);
+//  * PD planes of loads are in flight (registers), and workgroups take one column at a time.
+// Products and order are k_spmm_tpl3's (the slots the host check found unused in every
+// template -- the (z +- 1), (y +- 1) groups' neighbour halves -- would add +0.0, which leaves a
+// running sum that starts at +0.0 unchanged): the same bits.
+// -------------------------------------------------------------------------------------
+template <int PD, bool CS>
+__global__ __launch_bounds__(256) void k_spmm_march7(int npairs, int n_local, const unsigned char *__restrict__ tid,
+                                                     const unsigned long long *__restrict__ grp, int ntpl,
+                                                     MarchGeom mg, int txn, int tyn, int tzn, int sz,
+                                                     const double *__restrict__ vals, int nvals, MvDesc X, MvDesc Y,
+                                                     double alpha, double beta, const double *__restrict__ cs) {
+#pragma clang fp contract(off)
+  extern __shared__ __attribute__((aligned(16))) double march_lds[];
+  d2 *ring = (d2 *)march_lds;                          // [3][kMarchLY][kMarchLX]
+  double *s_coef = march_lds + 2 * 3 * kMarchPl;       // [ntpl][30]
+  unsigned *s_mask = (unsigned *)(s_coef + 30 * ntpl);  // [ntpl]: bit 6 g + i = slot i of group g used
+  const int t = threadIdx.x;
+  for (int e = t; e < 30 * ntpl; e += 256) {
+    const int tt = e / 30, r = e % 30;
+    const unsigned sl = (unsigned)(grp[tt * 5 + r / 6] >> (8 * (r % 6))) & 0xFF;
+    s_coef[e] = (sl != 0xFF && (int)sl < nvals) ? vals[sl] : 0.0;
+  }
+  for (int tt = t; tt < ntpl; tt += 256) {
+    unsigned m = 0;
+    for (int r = 0; r < 30; ++r) m |= (((unsigned)(grp[tt * 5 + r / 6] >> (8 * (r % 6))) & 0xFF) != 0xFF ? 1u : 0u) << r;
+    s_mask[tt] = m;
+  }
+  const int ntile = txn * tyn * tzn, per = (ntile + 7) >> 3;
+  const int tile = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+  if (tile >= ntile) return;  // uniform
+  const int ty = tile % tyn, tx = (tile / tyn) % txn, tz = tile / (tyn * txn);
+  const int lx = t & 63, ly = t >> 6;
+  int sx[2], sy[2], spos[2];
+  sx[0] = tx * kMarchTX + lx;
+  sy[0] = ty * kMarchTY + ly;
+  spos[0] = (ly + 1) * kMarchLX + lx + 1;
+  {
+    int line, xp;
+    if (t < 128) {
+      line = t < 64 ? 0 : kMarchLY - 1;
+      xp = lx + 1;
+    } else {
+      const int e = t - 128;
+      line = e >> 1;
+      xp = (e & 1) ? kMarchLX - 1 : 0;
+    }
+    sx[1] = tx * kMarchTX + xp - 1;
+    sy[1] = ty * kMarchTY + line - 1;
+    spos[1] = line * kMarchLX + xp;
+  }
+  bool sok[2];
+  int soff[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    sok[h] = (h == 0 || t < 140) && sx[h] >= 0 && sx[h] < mg.nxp && sy[h] >= 0 && sy[h] < mg.nyl;
+    soff[h] = sok[h] ? sy[h] * mg.nxp + sx[h] : 0;
+  }
+  const bool own = sok[0];
+  const int z0 = tz * sz, z1 = min(z0 + sz, mg.nz);
+  const int k = Y.ncols;
+  __syncthreads();  // coefficient table
+
+  double w[30];
+  unsigned msk = 0;
+  struct PlaneRegs {
+    d2 v[2];
+    d2 sc[CS ? 2 : 1];
+    int tid;
+  };
+  for (int c = 0; c < k; ++c) {
+    const double *xc = colp(X, c);
+    double *yc = colp(Y, c);
+    int tcoef = -1;
+    auto load = [&](PlaneRegs &r, int q) __attribute__((always_inline)) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const long long pr = (long long)q * mg.plane + soff[h];
+        const bool ok = sok[h] && q >= 0 && q < mg.nz && pr < npairs;
+        const long long pc = ok ? pr : 0;
+        r.v[h] = ok ? *(const d2 *)(xc + 2 * pc) : d2{0.0, 0.0};
+        if constexpr (CS) r.sc[h] = ok ? *(const d2 *)(cs + 2 * pc) : d2{0.0, 0.0};
+      }
+      const long long pr = (long long)q * mg.plane + soff[0];
+      r.tid = (own && q >= 0 && q < mg.nz && pr < npairs) ? (int)tid[pr] : 0xFF;
+    };
+    // plane q -> ring slot s (q's own scaled operand returned: the lane's (z +- 1) centre later)
+    auto stage = [&](const PlaneRegs &r, int s) __attribute__((always_inline)) {
+      d2 *d = ring + s * kMarchPl;
+      d2 o = r.v[0], o1 = r.v[1];
+      if constexpr (CS) {
+        o = r.sc[0] * r.v[0];
+        o1 = r.sc[CS ? 1 : 0] * r.v[1];
+      }
+      d[spos[0]] = o;
+      if (t < 140) d[spos[1]] = o1;
+      return o;
+    };
+    if (c > 0) march_barrier();  // the previous column's last plane has been read
+    PlaneRegs rb[PD];
+    d2 om, oz;  // own operands of planes z - 1 and z
+    {
+      PlaneRegs r0;
+      load(r0, z0 - 1);
+      om = r0.v[0];
+      if constexpr (CS) om = r0.sc[0] * r0.v[0];
+      load(r0, z0);
+      oz = stage(r0, z0 % 3);
+      int tc = r0.tid;
+#pragma unroll
+      for (int i = 0; i < PD; ++i) load(rb[i], z0 + 1 + i);
+      // plane z: stage z + 1 from rb[i] into slot (z + 1) % 3, refill rb[i] with plane z + 1 + PD,
+      // one barrier, then plane z's products (reading slot z % 3)
+      int sz3 = z0 % 3;
+      for (int z = z0; z < z1; z += PD) {
+#pragma unroll
+        for (int i = 0; i < PD; ++i) {
+          const int zz = z + i;
+          if (zz < z1) {
+            const int sn = sz3 == 2 ? 0 : sz3 + 1;
+            const d2 op = stage(rb[i], sn);
+            const int tzz = tc;
+            tc = rb[i].tid;
+            load(rb[i], zz + 1 + PD);
+            march_barrier();
+            if (own && tzz != 0xFF) {
+              if (tzz != tcoef) {
+#pragma unroll
+                for (int r = 0; r < 30; ++r) w[r] = s_coef[tzz * 30 + r];
+                msk = s_mask[tzz];
+                tcoef = tzz;
+              }
+              const d2 *b = ring + sz3 * kMarchPl + (ly + 1) * kMarchLX + lx + 1;
+              const d2 ym = b[-kMarchLX], yp = b[kMarchLX];
+              const double left = b[-1].y, right = b[1].x;
+              const d2 ctr[5] = {om, ym, oz, yp, op};
+              double sa = 0.0, sb = 0.0;
+#pragma unroll
+              for (int g = 0; g < 5; ++g) {
+                const d2 x = ctr[g];
+                if (g == 2) sa = sa + ((msk >> 12) & 1u ? w[12] * left : 0.0);
+                sa = sa + ((msk >> (6 * g + 1)) & 1u ? w[6 * g + 1] * x.x : 0.0);
+                sa = sa + ((msk >> (6 * g + 2)) & 1u ? w[6 * g + 2] * x.y : 0.0);
+                sb = sb + ((msk >> (6 * g + 3)) & 1u ? w[6 * g + 3] * x.x : 0.0);
+                sb = sb + ((msk >> (6 * g + 4)) & 1u ? w[6 * g + 4] * x.y : 0.0);
+                if (g == 2) sb = sb + ((msk >> 17) & 1u ? w[17] * right : 0.0);
+              }
+              const long long ra = 2 * ((long long)zz * mg.plane + soff[0]);
+              double *yq = yc + ra;
+              if (beta == 0.0) {
+                if (alpha != 1.0) {
+                  sa = alpha * sa;
+                  sb = alpha * sb;
+                }
+              } else {
+                sa = alpha * sa + beta * yq[0];
+                if (ra + 1 < n_local) sb = alpha * sb + beta * yq[1];
+              }
+              if (ra + 1 < n_local)
+                *(d2 *)yq = d2{sa, sb};
+              else
+                yq[0] = sa;
+            }
+            om = oz;
+            oz = op;
+            sz3 = sn;
+          }
+        }
+      }
+    }
+  }
+}
+
+bool launch_spmm_march7(hipStream_t s, int n_local, const unsigned char *tid, const unsigned long long *grp, int ntpl,
+                        const MarchGeom &geom, const double *vals, int nvals, MvDesc X, MvDesc Y, double alpha,
+                        double beta, const double *colscale, int sz, int pd) {
+  const int npairs = (n_local + 1) / 2;
+  if (npairs <= 0 || Y.ncols <= 0) return true;
+  if (geom.nxp <= 0 || geom.nyl <= 0 || geom.plane != geom.nxp * geom.nyl ||
+      (long long)geom.nz * geom.plane < npairs)
+    return false;
+  if (sz <= 0) {
+    static int cus = 0;
+    if (!cus) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        cus = 256;
+    }
+    const long long cols = (long long)cdiv(geom.nxp, kMarchTX) * cdiv(geom.nyl, kMarchTY);
+    const long long slabs = std::max(1LL, std::min((long long)cus * 3 / cols, (long long)cdiv(geom.nz, 8)));
+    sz = cdiv(geom.nz, slabs);
+  }
+  const int txn = cdiv(geom.nxp, kMarchTX), tyn = cdiv(geom.nyl, kMarchTY), tzn = cdiv(geom.nz, sz);
+  const int ntile = txn * tyn * tzn;
+  const size_t lds = sizeof(d2) * 3 * kMarchPl + sizeof(double) * 30 * ntpl + sizeof(unsigned) * ntpl;
+  const int grid = 8 * ((ntile + 7) / 8);
+#define M7(PD)                                                                                                       \
+  if (colscale)                                                                                                      \
+    k_spmm_march7<PD, true><<<grid, 256, lds, s>>>(npairs, n_local, tid, grp, ntpl, geom, txn, tyn, tzn, sz, vals,   \
+                                                   nvals, X, Y, alpha, beta, colscale);                              \
+  else                                                                                                               \
+    k_spmm_march7<PD, false><<<grid, 256, lds, s>>>(npairs, n_local, tid, grp, ntpl, geom, txn, tyn, tzn, sz, vals,  \
+                                                    nvals, X, Y, alpha, beta, colscale)
+  if (pd >= 4) {
+    M7(4);
+  } else if (pd == 3) {
+    M7(3);
+  } else if (pd == 2) {
+    M7(2);
+  } else {
+    M7(1);
+  }
+#undef M7
   LAUNCH_CHECK();
   return true;
 }

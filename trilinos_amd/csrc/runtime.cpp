@@ -815,12 +815,30 @@ static void setup_template_kernels(migmres_crs *A, const PairTemplates &pt) {
     A->tpl3_center = sg.center;
     A->tpl3_G = sg.G;
   };
-  // the plane march (k_spmm_march) for 3-D stencil groups; MIGMRES_NO_MARCH=1 keeps the
-  // template kernels
+  // the plane march for 3-D stencil groups: k_spmm_march7 for the 7-point pattern (measured
+  // faster than the template kernel); the general k_spmm_march (any 3-D groups) only with
+  // MIGMRES_MARCH_GENERIC=1 -- for 27 points it is slower than the lane-shared k_spmm_tpl3
+  // (its LDS reads bound it).  MIGMRES_NO_MARCH=1 keeps the template kernels.
   MarchGeometry mg;
-  if (!env_on("MIGMRES_NO_MARCH") && groups && make_march_geometry(sg, pt.ntpl, pt.npairs, mg) &&
+  const bool generic = env_on("MIGMRES_MARCH_GENERIC");
+  bool seven = groups && sg.G == 5;
+  if (!env_on("MIGMRES_NO_MARCH") && groups && make_march_geometry(sg, pt.ntpl, pt.npairs, mg)) {
+    if (seven) {
+      static const int want_a[5] = {-1, 0, 0, 0, 1}, want_b[5] = {0, -1, 0, 1, 0};
+      for (int g = 0; g < 5; ++g) seven = seven && mg.ga[(size_t)g] == want_a[g] && mg.gb[(size_t)g] == want_b[g];
+      // neighbour halves only on the x line
+      for (int t = 0; t < pt.ntpl && seven; ++t)
+        for (int g = 0; g < 5; ++g)
+          if (g != 2) {
+            const unsigned long long w = sg.slots[(size_t)t * 5 + g];
+            seven = seven && (w & 0xFF) == kTplUnused && ((w >> 40) & 0xFF) == kTplUnused;
+          }
+    }
+  }
+  if (!env_on("MIGMRES_NO_MARCH") && groups && (generic || seven) && mg.nxp > 0 &&
       march_check(A->ctx->stream, pt.npairs, A->d_tpl_id, (const int4 *)mg.tb.data(), pt.ntpl, mg.nxp, mg.nyl) == 0) {
     upload_groups();
+    A->use_march7 = seven && !generic;
     A->march.nxp = mg.nxp;
     A->march.nyl = mg.nyl;
     A->march.plane = mg.plane;
@@ -834,6 +852,8 @@ static void setup_template_kernels(migmres_crs *A, const PairTemplates &pt) {
     A->march_kc = kc ? std::atoi(kc) : 2;
     const char *sz = std::getenv("MIGMRES_MARCH_SZ");
     A->march_sz = sz ? std::atoi(sz) : 0;
+    const char *pd = std::getenv("MIGMRES_MARCH_PD");
+    A->march_pd = pd ? std::atoi(pd) : (A->use_march7 ? 2 : 1);
     return;
   }
   if (!env_on("MIGMRES_NO_TPL3") && (pt.maxk > 12 || short_ok) && groups) {
@@ -1211,9 +1231,12 @@ static void crs_apply_impl(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, d
   if (A.use_tpl) {
     // templated pairs read no ghost column: they run while the halo is in flight, then the
     // pairs that do read one go to the fallback kernel
-    bool done = A.use_march && launch_spmm_march(c->stream, A.n_local, A.d_tpl_id, A.d_tpl3_grp, A.tpl_ntpl,
-                                                 A.tpl3_G, A.march, A.d_tpl_val, A.tpl_nvals, X.desc(), Y.desc(),
-                                                 alpha, beta, cs.own, A.march_kc, A.march_sz);
+    bool done = A.use_march7 ? launch_spmm_march7(c->stream, A.n_local, A.d_tpl_id, A.d_tpl3_grp, A.tpl_ntpl,
+                                                  A.march, A.d_tpl_val, A.tpl_nvals, X.desc(), Y.desc(), alpha,
+                                                  beta, cs.own, A.march_sz, A.march_pd)
+                : A.use_march && launch_spmm_march(c->stream, A.n_local, A.d_tpl_id, A.d_tpl3_grp, A.tpl_ntpl,
+                                                   A.tpl3_G, A.march, A.d_tpl_val, A.tpl_nvals, X.desc(), Y.desc(),
+                                                   alpha, beta, cs.own, A.march_kc, A.march_sz, A.march_pd);
     done = done || (A.use_tpl3 && launch_spmm_tpl3(c->stream, A.n_local, A.d_tpl_id, A.d_tpl3_grp, A.tpl_ntpl,
                                                    A.tpl3_G, A.tpl3_center.data(), A.d_tpl_val, A.tpl_nvals,
                                                    X.desc(), Y.desc(), alpha, beta, cs.own, A.tpl3_slabs,

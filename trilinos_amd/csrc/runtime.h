@@ -177,7 +177,8 @@ struct migmres_crs {
   // that every templated pair fits (make_march_geometry + march_check)
   migmres::MarchGeom march;
   bool use_march = false;
-  int march_kc = 2, march_sz = 0;  // columns staged per plane, planes per slab (0: auto)
+  bool use_march7 = false;  // the 7-point specialisation (k_spmm_march7)
+  int march_kc = 2, march_sz = 0, march_pd = 1;  // columns per staged plane, planes per slab (0: auto), planes prefetched
   int tpl_slabs = 0, tpl_kc = 8;
   int n_tpl_rest = 0;
   double spmm_fixed_bytes = 0.0;  // matrix-format bytes one apply reads (bench accounting)
