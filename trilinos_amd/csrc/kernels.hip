@@ -1331,9 +1331,12 @@ __global__ __launch_bounds__(256) void k_spmm_march7(int npairs, int n_local, co
     for (int r = 0; r < 30; ++r) m |= (((unsigned)(grp[tt * 5 + r / 6] >> (8 * (r % 6))) & 0xFF) != 0xFF ? 1u : 0u) << r;
     s_mask[tt] = m;
   }
-  const int ntile = txn * tyn * tzn, per = (ntile + 7) >> 3;
-  const int tile = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
-  if (tile >= ntile) return;  // uniform
+  // work item = (column, tile): XCD b mod 8 takes the b-th eighth, lines fastest, so a tile's
+  // line halo was usually just loaded by its neighbour on the same XCD
+  const int ntile = txn * tyn * tzn, nwork = ntile * Y.ncols, per = (nwork + 7) >> 3;
+  const int work = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+  if (work >= nwork) return;  // uniform
+  const int c = work / ntile, tile = work % ntile;
   const int ty = tile % tyn, tx = (tile / tyn) % txn, tz = tile / (tyn * txn);
   const int lx = t & 63, ly = t >> 6;
   int sx[2], sy[2], spos[2];
@@ -1363,7 +1366,6 @@ __global__ __launch_bounds__(256) void k_spmm_march7(int npairs, int n_local, co
   }
   const bool own = sok[0];
   const int z0 = tz * sz, z1 = min(z0 + sz, mg.nz);
-  const int k = Y.ncols;
   __syncthreads();  // coefficient table
 
   double w[30];
@@ -1373,7 +1375,7 @@ __global__ __launch_bounds__(256) void k_spmm_march7(int npairs, int n_local, co
     d2 sc[CS ? 2 : 1];
     int tid;
   };
-  for (int c = 0; c < k; ++c) {
+  {
     const double *xc = colp(X, c);
     double *yc = colp(Y, c);
     int tcoef = -1;
@@ -1401,7 +1403,6 @@ __global__ __launch_bounds__(256) void k_spmm_march7(int npairs, int n_local, co
       if (t < 140) d[spos[1]] = o1;
       return o;
     };
-    if (c > 0) march_barrier();  // the previous column's last plane has been read
     PlaneRegs rb[PD];
     d2 om, oz;  // own operands of planes z - 1 and z
     {
@@ -1492,12 +1493,14 @@ bool launch_spmm_march7(hipStream_t s, int n_local, const unsigned char *tid, co
           hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
         cus = 256;
     }
-    const long long cols = (long long)cdiv(geom.nxp, kMarchTX) * cdiv(geom.nyl, kMarchTY);
-    const long long slabs = std::max(1LL, std::min((long long)cus * 3 / cols, (long long)cdiv(geom.nz, 8)));
+    // slabs: about three rounds of resident workgroups (3 per CU) over all (column, tile) work
+    // items, at least 4 planes per slab (each slab re-reads 2 halo planes)
+    const long long cols = (long long)cdiv(geom.nxp, kMarchTX) * cdiv(geom.nyl, kMarchTY) * Y.ncols;
+    const long long slabs = std::max(1LL, std::min((long long)cdiv(9LL * cus, cols), (long long)cdiv(geom.nz, 4)));
     sz = cdiv(geom.nz, slabs);
   }
   const int txn = cdiv(geom.nxp, kMarchTX), tyn = cdiv(geom.nyl, kMarchTY), tzn = cdiv(geom.nz, sz);
-  const int ntile = txn * tyn * tzn;
+  const int ntile = txn * tyn * tzn * Y.ncols;
   const size_t lds = sizeof(d2) * 3 * kMarchPl + sizeof(double) * 30 * ntpl + sizeof(unsigned) * ntpl;
   const int grid = 8 * ((ntile + 7) / 8);
 #define M7(PD)                                                                                                       \
