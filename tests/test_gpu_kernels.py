@@ -434,15 +434,24 @@ def test_spmm_march_bit_exact(comm, kind, dims, k, alpha, beta, generic, monkeyp
     assert np.array_equal(Yd.download(), want)
 
 
-@pytest.mark.parametrize("kind,generic,kc,sz,pd", [("Laplace3D", False, "1", "1", "1"), ("Laplace3D", False, "1", "3", "2"),
-                                                   ("Laplace3D", False, "1", "5", "3"), ("Laplace3D", False, "1", "64", "4"),
-                                                   ("Laplace3D", False, "1", "2", "4"), ("Laplace3D", True, "1", "1", "1"),
-                                                   ("Laplace3D", True, "2", "5", "2"), ("Brick3D", True, "1", "3", "2"),
-                                                   ("Brick3D", True, "2", "2", "1"), ("Brick3D", True, "2", "64", "2")])
-def test_spmm_march_slabs_bit_exact(comm, kind, generic, kc, sz, pd, monkeypatch):
+@pytest.mark.parametrize("kind,generic,kc,sz,pd,nl", [("Laplace3D", False, "1", "1", "1", "1"),
+                                                      ("Laplace3D", False, "1", "3", "2", "1"),
+                                                      ("Laplace3D", False, "1", "5", "3", "1"),
+                                                      ("Laplace3D", False, "1", "64", "3", "2"),
+                                                      ("Laplace3D", False, "1", "2", "2", "2"),
+                                                      ("Laplace3D", False, "1", "1", "1", "2"),
+                                                      ("Laplace3D", False, "1", "4", "3", "2"),
+                                                      ("Laplace3D", True, "1", "1", "1", "1"),
+                                                      ("Laplace3D", True, "2", "5", "2", "1"),
+                                                      ("Brick3D", True, "1", "3", "2", "1"),
+                                                      ("Brick3D", True, "2", "2", "1", "1"),
+                                                      ("Brick3D", True, "2", "64", "2", "1")])
+@pytest.mark.parametrize("dims", [(14, 9, 11), (140, 13, 6)])
+def test_spmm_march_slabs_bit_exact(comm, kind, generic, kc, sz, pd, nl, dims, monkeypatch):
     """The march's walk knobs -- MIGMRES_MARCH_SZ planes per workgroup (one plane, ragged last
-    slabs, one slab for all), MIGMRES_MARCH_PD planes of loads in flight, MIGMRES_MARCH_KC
-    columns per staged plane (general form) -- change only the walk: same bits as the oracle."""
+    slabs, one slab for all), MIGMRES_MARCH_PD planes of loads in flight, MIGMRES_MARCH_NL lines
+    per thread (tiles of 4 or 8 lines), MIGMRES_MARCH_KC columns per staged plane (general
+    form) -- change only the walk: same bits as the oracle."""
     import trilinos_amd as ta
     from oracle import epetra as oe
     if generic:
@@ -450,7 +459,8 @@ def test_spmm_march_slabs_bit_exact(comm, kind, generic, kc, sz, pd, monkeypatch
     monkeypatch.setenv("MIGMRES_MARCH_KC", kc)
     monkeypatch.setenv("MIGMRES_MARCH_SZ", sz)
     monkeypatch.setenv("MIGMRES_MARCH_PD", pd)
-    nx, ny, nz, k = 14, 9, 11, 5
+    monkeypatch.setenv("MIGMRES_MARCH_NL", nl)
+    (nx, ny, nz), k = dims, 5
     n = nx * ny * nz
     A = ta.CrsMatrix.galeri(comm, kind, nx, ny, nz)
     assert A.spmm_kernel() == "march"

@@ -127,10 +127,11 @@ bool launch_spmm_march(hipStream_t s, int n_local, const unsigned char *tid, con
                        double beta, const double *colscale = nullptr, int kcmax = 2, int sz = 0, int pd = 1);
 // The march for the 7-point pattern (G = 5: groups (z - 1), (y - 1), x line, (y + 1), (z + 1)
 // with neighbour halves only on the x line): coefficients in registers, only plane z staged,
-// the (z +- 1) centres from the lane's own loads; pd planes of loads in flight (1..4).
+// the (z +- 1) centres from the lane's own loads; pd planes of loads in flight (1..3), nl lines
+// per thread (1, 2: tiles of 4 nl lines).
 bool launch_spmm_march7(hipStream_t s, int n_local, const unsigned char *tid, const unsigned long long *grp, int ntpl,
                         const MarchGeom &geom, const double *vals, int nvals, MvDesc X, MvDesc Y, double alpha,
-                        double beta, const double *colscale = nullptr, int sz = 0, int pd = 2);
+                        double beta, const double *colscale = nullptr, int sz = 0, int pd = 2, int nl = 1);
 // Number of templated pairs that the march geometry cannot serve (a used x-neighbour half
 // across a line end, a group line outside the plane).  tbounds: per template {needs x-1 half,
 // needs x+1 half, lowest group line offset, highest}.

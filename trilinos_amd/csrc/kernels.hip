@@ -1309,16 +1309,18 @@ bool launch_spmm_march(hipStream_t s, int n_local, const unsigned char *tid, con
 // template -- the (z +- 1), (y +- 1) groups' neighbour halves -- would add +0.0, which leaves a
 // running sum that starts at +0.0 unchanged): the same bits.
 // -------------------------------------------------------------------------------------
-template <int PD, bool CS>
+template <int PD, bool CS, int NL>
 __global__ __launch_bounds__(256) void k_spmm_march7(int npairs, int n_local, const unsigned char *__restrict__ tid,
                                                      const unsigned long long *__restrict__ grp, int ntpl,
                                                      MarchGeom mg, int txn, int tyn, int tzn, int sz,
                                                      const double *__restrict__ vals, int nvals, MvDesc X, MvDesc Y,
                                                      double alpha, double beta, const double *__restrict__ cs) {
 #pragma clang fp contract(off)
+  // NL lines per thread: tile of 64 pairs x 4 NL lines, staged with a one-pair / one-line halo
+  constexpr int TY = 4 * NL, LY = TY + 2, PL = LY * kMarchLX, NH = 128 + 2 * LY, NS = NL + 1;
   extern __shared__ __attribute__((aligned(16))) double march_lds[];
-  d2 *ring = (d2 *)march_lds;                          // [3][kMarchLY][kMarchLX]
-  double *s_coef = march_lds + 2 * 3 * kMarchPl;       // [ntpl][30]
+  d2 *ring = (d2 *)march_lds;                          // [3][LY][kMarchLX]
+  double *s_coef = march_lds + 2 * 3 * PL;             // [ntpl][30]
   unsigned *s_mask = (unsigned *)(s_coef + 30 * ntpl);  // [ntpl]: bit 6 g + i = slot i of group g used
   const int t = threadIdx.x;
   for (int e = t; e < 30 * ntpl; e += 256) {
@@ -1339,139 +1341,150 @@ __global__ __launch_bounds__(256) void k_spmm_march7(int npairs, int n_local, co
   const int c = work / ntile, tile = work % ntile;
   const int ty = tile % tyn, tx = (tile / tyn) % txn, tz = tile / (tyn * txn);
   const int lx = t & 63, ly = t >> 6;
-  int sx[2], sy[2], spos[2];
-  sx[0] = tx * kMarchTX + lx;
-  sy[0] = ty * kMarchTY + ly;
-  spos[0] = (ly + 1) * kMarchLX + lx + 1;
-  {
+  // load slots: i < NL this thread's own pair on tile line ly + 4 i; NL: a halo pair (t < NH:
+  // the two halo lines, then the left / right halo pair of each staged line)
+  int spos[NS], soff[NS];
+  bool sok[NS];
+#pragma unroll
+  for (int i = 0; i < NS; ++i) {
     int line, xp;
-    if (t < 128) {
-      line = t < 64 ? 0 : kMarchLY - 1;
+    if (i < NL) {
+      line = ly + 4 * i + 1;
+      xp = lx + 1;
+    } else if (t < 128) {
+      line = t < 64 ? 0 : LY - 1;
       xp = lx + 1;
     } else {
       const int e = t - 128;
       line = e >> 1;
       xp = (e & 1) ? kMarchLX - 1 : 0;
     }
-    sx[1] = tx * kMarchTX + xp - 1;
-    sy[1] = ty * kMarchTY + line - 1;
-    spos[1] = line * kMarchLX + xp;
+    const int gx = tx * kMarchTX + xp - 1, gy = ty * TY + line - 1;
+    sok[i] = (i < NL || t < NH) && gx >= 0 && gx < mg.nxp && gy >= 0 && gy < mg.nyl;
+    soff[i] = sok[i] ? gy * mg.nxp + gx : 0;
+    spos[i] = line * kMarchLX + xp;
   }
-  bool sok[2];
-  int soff[2];
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    sok[h] = (h == 0 || t < 140) && sx[h] >= 0 && sx[h] < mg.nxp && sy[h] >= 0 && sy[h] < mg.nyl;
-    soff[h] = sok[h] ? sy[h] * mg.nxp + sx[h] : 0;
-  }
-  const bool own = sok[0];
   const int z0 = tz * sz, z1 = min(z0 + sz, mg.nz);
   __syncthreads();  // coefficient table
 
   double w[30];
   unsigned msk = 0;
+  int tcoef = -1;
   struct PlaneRegs {
-    d2 v[2];
-    d2 sc[CS ? 2 : 1];
-    int tid;
+    d2 v[NS];
+    d2 sc[CS ? NS : 1];
+    int tid[NL];
   };
+  const double *xc = colp(X, c);
+  double *yc = colp(Y, c);
+  auto load = [&](PlaneRegs &r, int q) __attribute__((always_inline)) {
+#pragma unroll
+    for (int h = 0; h < NS; ++h) {
+      const long long pr = (long long)q * mg.plane + soff[h];
+      const bool ok = sok[h] && q >= 0 && q < mg.nz && pr < npairs;
+      const long long pc = ok ? pr : 0;
+      r.v[h] = ok ? *(const d2 *)(xc + 2 * pc) : d2{0.0, 0.0};
+      if constexpr (CS) r.sc[h] = ok ? *(const d2 *)(cs + 2 * pc) : d2{0.0, 0.0};
+    }
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const long long pr = (long long)q * mg.plane + soff[i];
+      r.tid[i] = (sok[i] && q >= 0 && q < mg.nz && pr < npairs) ? (int)tid[pr] : 0xFF;
+    }
+  };
+  auto operand = [&](const PlaneRegs &r, int h) __attribute__((always_inline)) {
+    d2 o = r.v[h];
+    if constexpr (CS) o = r.sc[h] * r.v[h];
+    return o;
+  };
+  // plane q -> ring slot s; the own lines' (scaled) operands go to o (the lanes' z +- 1 centres)
+  auto stage = [&](const PlaneRegs &r, int s, d2 (&o)[NL]) __attribute__((always_inline)) {
+    d2 *d = ring + s * PL;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      o[i] = operand(r, i);
+      d[spos[i]] = o[i];
+    }
+    if (t < NH) d[spos[NL]] = operand(r, NL);
+  };
+  PlaneRegs rb[PD];
+  d2 om[NL], oz[NL], op[NL];  // own operands of planes z - 1, z, z + 1
+  int tc[NL];
   {
-    const double *xc = colp(X, c);
-    double *yc = colp(Y, c);
-    int tcoef = -1;
-    auto load = [&](PlaneRegs &r, int q) __attribute__((always_inline)) {
+    PlaneRegs r0;
+    load(r0, z0 - 1);
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const long long pr = (long long)q * mg.plane + soff[h];
-        const bool ok = sok[h] && q >= 0 && q < mg.nz && pr < npairs;
-        const long long pc = ok ? pr : 0;
-        r.v[h] = ok ? *(const d2 *)(xc + 2 * pc) : d2{0.0, 0.0};
-        if constexpr (CS) r.sc[h] = ok ? *(const d2 *)(cs + 2 * pc) : d2{0.0, 0.0};
-      }
-      const long long pr = (long long)q * mg.plane + soff[0];
-      r.tid = (own && q >= 0 && q < mg.nz && pr < npairs) ? (int)tid[pr] : 0xFF;
-    };
-    // plane q -> ring slot s (q's own scaled operand returned: the lane's (z +- 1) centre later)
-    auto stage = [&](const PlaneRegs &r, int s) __attribute__((always_inline)) {
-      d2 *d = ring + s * kMarchPl;
-      d2 o = r.v[0], o1 = r.v[1];
-      if constexpr (CS) {
-        o = r.sc[0] * r.v[0];
-        o1 = r.sc[CS ? 1 : 0] * r.v[1];
-      }
-      d[spos[0]] = o;
-      if (t < 140) d[spos[1]] = o1;
-      return o;
-    };
-    PlaneRegs rb[PD];
-    d2 om, oz;  // own operands of planes z - 1 and z
-    {
-      PlaneRegs r0;
-      load(r0, z0 - 1);
-      om = r0.v[0];
-      if constexpr (CS) om = r0.sc[0] * r0.v[0];
-      load(r0, z0);
-      oz = stage(r0, z0 % 3);
-      int tc = r0.tid;
+    for (int i = 0; i < NL; ++i) om[i] = operand(r0, i);
+    load(r0, z0);
+    stage(r0, z0 % 3, oz);
 #pragma unroll
-      for (int i = 0; i < PD; ++i) load(rb[i], z0 + 1 + i);
-      // plane z: stage z + 1 from rb[i] into slot (z + 1) % 3, refill rb[i] with plane z + 1 + PD,
-      // one barrier, then plane z's products (reading slot z % 3)
-      int sz3 = z0 % 3;
-      for (int z = z0; z < z1; z += PD) {
+    for (int i = 0; i < NL; ++i) tc[i] = r0.tid[i];
+  }
 #pragma unroll
-        for (int i = 0; i < PD; ++i) {
-          const int zz = z + i;
-          if (zz < z1) {
-            const int sn = sz3 == 2 ? 0 : sz3 + 1;
-            const d2 op = stage(rb[i], sn);
-            const int tzz = tc;
-            tc = rb[i].tid;
-            load(rb[i], zz + 1 + PD);
-            march_barrier();
-            if (own && tzz != 0xFF) {
-              if (tzz != tcoef) {
+  for (int i = 0; i < PD; ++i) load(rb[i], z0 + 1 + i);
+  // plane z: stage z + 1 from rb[i] into slot (z + 1) % 3, refill rb[i] with plane z + 1 + PD,
+  // one barrier, then plane z's products (reading slot z % 3)
+  int sz3 = z0 % 3;
+  for (int z = z0; z < z1; z += PD) {
 #pragma unroll
-                for (int r = 0; r < 30; ++r) w[r] = s_coef[tzz * 30 + r];
-                msk = s_mask[tzz];
-                tcoef = tzz;
-              }
-              const d2 *b = ring + sz3 * kMarchPl + (ly + 1) * kMarchLX + lx + 1;
-              const d2 ym = b[-kMarchLX], yp = b[kMarchLX];
-              const double left = b[-1].y, right = b[1].x;
-              const d2 ctr[5] = {om, ym, oz, yp, op};
-              double sa = 0.0, sb = 0.0;
+    for (int i = 0; i < PD; ++i) {
+      const int zz = z + i;
+      if (zz < z1) {
+        const int sn = sz3 == 2 ? 0 : sz3 + 1;
+        stage(rb[i], sn, op);
+        int tzz[NL];
 #pragma unroll
-              for (int g = 0; g < 5; ++g) {
-                const d2 x = ctr[g];
-                if (g == 2) sa = sa + ((msk >> 12) & 1u ? w[12] * left : 0.0);
-                sa = sa + ((msk >> (6 * g + 1)) & 1u ? w[6 * g + 1] * x.x : 0.0);
-                sa = sa + ((msk >> (6 * g + 2)) & 1u ? w[6 * g + 2] * x.y : 0.0);
-                sb = sb + ((msk >> (6 * g + 3)) & 1u ? w[6 * g + 3] * x.x : 0.0);
-                sb = sb + ((msk >> (6 * g + 4)) & 1u ? w[6 * g + 4] * x.y : 0.0);
-                if (g == 2) sb = sb + ((msk >> 17) & 1u ? w[17] * right : 0.0);
-              }
-              const long long ra = 2 * ((long long)zz * mg.plane + soff[0]);
-              double *yq = yc + ra;
-              if (beta == 0.0) {
-                if (alpha != 1.0) {
-                  sa = alpha * sa;
-                  sb = alpha * sb;
-                }
-              } else {
-                sa = alpha * sa + beta * yq[0];
-                if (ra + 1 < n_local) sb = alpha * sb + beta * yq[1];
-              }
-              if (ra + 1 < n_local)
-                *(d2 *)yq = d2{sa, sb};
-              else
-                yq[0] = sa;
-            }
-            om = oz;
-            oz = op;
-            sz3 = sn;
-          }
+        for (int l = 0; l < NL; ++l) {
+          tzz[l] = tc[l];
+          tc[l] = rb[i].tid[l];
         }
+        load(rb[i], zz + 1 + PD);
+        march_barrier();
+#pragma unroll
+        for (int l = 0; l < NL; ++l) {
+          const int tl = tzz[l];
+          if (tl != 0xFF) {
+            if (tl != tcoef) {  // the lines of a tile share a template away from the grid edges
+#pragma unroll
+              for (int r = 0; r < 30; ++r) w[r] = s_coef[tl * 30 + r];
+              msk = s_mask[tl];
+              tcoef = tl;
+            }
+            const d2 *b = ring + sz3 * PL + spos[l];
+            const d2 ym = b[-kMarchLX], yp = b[kMarchLX];
+            const double left = b[-1].y, right = b[1].x;
+            const d2 ctr[5] = {om[l], ym, oz[l], yp, op[l]};
+            double sa = 0.0, sb = 0.0;
+#pragma unroll
+            for (int g = 0; g < 5; ++g) {
+              const d2 x = ctr[g];
+              if (g == 2) sa = sa + ((msk >> 12) & 1u ? w[12] * left : 0.0);
+              sa = sa + ((msk >> (6 * g + 1)) & 1u ? w[6 * g + 1] * x.x : 0.0);
+              sa = sa + ((msk >> (6 * g + 2)) & 1u ? w[6 * g + 2] * x.y : 0.0);
+              sb = sb + ((msk >> (6 * g + 3)) & 1u ? w[6 * g + 3] * x.x : 0.0);
+              sb = sb + ((msk >> (6 * g + 4)) & 1u ? w[6 * g + 4] * x.y : 0.0);
+              if (g == 2) sb = sb + ((msk >> 17) & 1u ? w[17] * right : 0.0);
+            }
+            const long long ra = 2 * ((long long)zz * mg.plane + soff[l]);
+            double *yq = yc + ra;
+            if (beta == 0.0) {
+              if (alpha != 1.0) {
+                sa = alpha * sa;
+                sb = alpha * sb;
+              }
+            } else {
+              sa = alpha * sa + beta * yq[0];
+              if (ra + 1 < n_local) sb = alpha * sb + beta * yq[1];
+            }
+            if (ra + 1 < n_local)
+              *(d2 *)yq = d2{sa, sb};
+            else
+              yq[0] = sa;
+          }
+          om[l] = oz[l];
+          oz[l] = op[l];
+        }
+        sz3 = sn;
       }
     }
   }
@@ -1479,12 +1492,14 @@ __global__ __launch_bounds__(256) void k_spmm_march7(int npairs, int n_local, co
 
 bool launch_spmm_march7(hipStream_t s, int n_local, const unsigned char *tid, const unsigned long long *grp, int ntpl,
                         const MarchGeom &geom, const double *vals, int nvals, MvDesc X, MvDesc Y, double alpha,
-                        double beta, const double *colscale, int sz, int pd) {
+                        double beta, const double *colscale, int sz, int pd, int nl) {
   const int npairs = (n_local + 1) / 2;
   if (npairs <= 0 || Y.ncols <= 0) return true;
   if (geom.nxp <= 0 || geom.nyl <= 0 || geom.plane != geom.nxp * geom.nyl ||
       (long long)geom.nz * geom.plane < npairs)
     return false;
+  nl = nl == 2 ? 2 : 1;
+  const int TY = 4 * nl;
   if (sz <= 0) {
     static int cus = 0;
     if (!cus) {
@@ -1495,29 +1510,38 @@ bool launch_spmm_march7(hipStream_t s, int n_local, const unsigned char *tid, co
     }
     // slabs: about three rounds of resident workgroups (3 per CU) over all (column, tile) work
     // items, at least 4 planes per slab (each slab re-reads 2 halo planes)
-    const long long cols = (long long)cdiv(geom.nxp, kMarchTX) * cdiv(geom.nyl, kMarchTY) * Y.ncols;
+    const long long cols = (long long)cdiv(geom.nxp, kMarchTX) * cdiv(geom.nyl, TY) * Y.ncols;
     const long long slabs = std::max(1LL, std::min((long long)cdiv(9LL * cus, cols), (long long)cdiv(geom.nz, 4)));
     sz = cdiv(geom.nz, slabs);
   }
-  const int txn = cdiv(geom.nxp, kMarchTX), tyn = cdiv(geom.nyl, kMarchTY), tzn = cdiv(geom.nz, sz);
+  const int txn = cdiv(geom.nxp, kMarchTX), tyn = cdiv(geom.nyl, TY), tzn = cdiv(geom.nz, sz);
   const int ntile = txn * tyn * tzn * Y.ncols;
-  const size_t lds = sizeof(d2) * 3 * kMarchPl + sizeof(double) * 30 * ntpl + sizeof(unsigned) * ntpl;
+  const size_t lds =
+      sizeof(d2) * 3 * (TY + 2) * kMarchLX + sizeof(double) * 30 * ntpl + sizeof(unsigned) * ntpl;
   const int grid = 8 * ((ntile + 7) / 8);
-#define M7(PD)                                                                                                       \
-  if (colscale)                                                                                                      \
-    k_spmm_march7<PD, true><<<grid, 256, lds, s>>>(npairs, n_local, tid, grp, ntpl, geom, txn, tyn, tzn, sz, vals,   \
-                                                   nvals, X, Y, alpha, beta, colscale);                              \
-  else                                                                                                               \
-    k_spmm_march7<PD, false><<<grid, 256, lds, s>>>(npairs, n_local, tid, grp, ntpl, geom, txn, tyn, tzn, sz, vals,  \
-                                                    nvals, X, Y, alpha, beta, colscale)
-  if (pd >= 4) {
-    M7(4);
-  } else if (pd == 3) {
-    M7(3);
-  } else if (pd == 2) {
-    M7(2);
+#define M7(PD, NL)                                                                                                    \
+  if (colscale)                                                                                                       \
+    k_spmm_march7<PD, true, NL><<<grid, 256, lds, s>>>(npairs, n_local, tid, grp, ntpl, geom, txn, tyn, tzn, sz,     \
+                                                       vals, nvals, X, Y, alpha, beta, colscale);                    \
+  else                                                                                                                \
+    k_spmm_march7<PD, false, NL><<<grid, 256, lds, s>>>(npairs, n_local, tid, grp, ntpl, geom, txn, tyn, tzn, sz,    \
+                                                        vals, nvals, X, Y, alpha, beta, colscale)
+  if (nl == 2) {
+    if (pd >= 3) {
+      M7(3, 2);
+    } else if (pd == 2) {
+      M7(2, 2);
+    } else {
+      M7(1, 2);
+    }
   } else {
-    M7(1);
+    if (pd >= 3) {
+      M7(3, 1);
+    } else if (pd == 2) {
+      M7(2, 1);
+    } else {
+      M7(1, 1);
+    }
   }
 #undef M7
   LAUNCH_CHECK();

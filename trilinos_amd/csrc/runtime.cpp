@@ -853,7 +853,9 @@ static void setup_template_kernels(migmres_crs *A, const PairTemplates &pt) {
     const char *sz = std::getenv("MIGMRES_MARCH_SZ");
     A->march_sz = sz ? std::atoi(sz) : 0;
     const char *pd = std::getenv("MIGMRES_MARCH_PD");
-    A->march_pd = pd ? std::atoi(pd) : (A->use_march7 ? 2 : 1);
+    A->march_pd = pd ? std::atoi(pd) : (A->use_march7 ? 3 : 1);
+    const char *nl = std::getenv("MIGMRES_MARCH_NL");
+    A->march_nl = nl ? std::atoi(nl) : 1;
     return;
   }
   if (!env_on("MIGMRES_NO_TPL3") && (pt.maxk > 12 || short_ok) && groups) {
@@ -1233,7 +1235,7 @@ static void crs_apply_impl(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, d
     // pairs that do read one go to the fallback kernel
     bool done = A.use_march7 ? launch_spmm_march7(c->stream, A.n_local, A.d_tpl_id, A.d_tpl3_grp, A.tpl_ntpl,
                                                   A.march, A.d_tpl_val, A.tpl_nvals, X.desc(), Y.desc(), alpha,
-                                                  beta, cs.own, A.march_sz, A.march_pd)
+                                                  beta, cs.own, A.march_sz, A.march_pd, A.march_nl)
                 : A.use_march && launch_spmm_march(c->stream, A.n_local, A.d_tpl_id, A.d_tpl3_grp, A.tpl_ntpl,
                                                    A.tpl3_G, A.march, A.d_tpl_val, A.tpl_nvals, X.desc(), Y.desc(),
                                                    alpha, beta, cs.own, A.march_kc, A.march_sz, A.march_pd);

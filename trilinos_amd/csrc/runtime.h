@@ -178,7 +178,7 @@ struct migmres_crs {
   migmres::MarchGeom march;
   bool use_march = false;
   bool use_march7 = false;  // the 7-point specialisation (k_spmm_march7)
-  int march_kc = 2, march_sz = 0, march_pd = 1;  // columns per staged plane, planes per slab (0: auto), planes prefetched
+  int march_kc = 2, march_sz = 0, march_pd = 1, march_nl = 1;  // columns per staged plane, planes per slab (0: auto), planes prefetched
   int tpl_slabs = 0, tpl_kc = 8;
   int n_tpl_rest = 0;
   double spmm_fixed_bytes = 0.0;  // matrix-format bytes one apply reads (bench accounting)
