@@ -84,7 +84,7 @@ def test_device_formats_equal_host_formats(kind, dims, P, monkeypatch):
         assert h[1] == d[1], "device-built format plans differ from the host builders'"
         assert h[1] == f[1], "device FillComplete + device formats differ from the host path"
     if P == 1:
-        expect = {"Laplace3D": "tpl", "Laplace2D": "tpl", "Brick3D": "tpl3", "FlanProxy": "bsr3",
+        expect = {"Laplace3D": "march", "Laplace2D": "tpl", "Brick3D": "march", "FlanProxy": "bsr3",
                   "noisy3D": "pair", "banded": "sell"}.get(kind)
         if expect:
             assert host[0][0] == expect

@@ -412,9 +412,9 @@ def test_spmm_bsr3_detects_not_assumes(comm):
 def test_spmm_march_bit_exact(comm, kind, dims, k, alpha, beta, generic, monkeypatch):
     """The 2.5-D plane march (plane tiles of 64 pairs x 4 lines staged in LDS; partial x tiles
     at nx = 130 / 134, partial line tiles, a few planes, odd column counts): by default the
-    7-point specialisation for Laplace3D (the 27-point operator keeps the lane-shared template
-    kernel), with MIGMRES_MARCH_GENERIC=1 the general form for both -- bit for bit against
-    the oracle, and Y = alpha A X + beta Y."""
+    7-point specialisation for Laplace3D and the uniform 27-point one for Brick3D, with
+    MIGMRES_MARCH_GENERIC=1 the general form for both -- bit for bit against the oracle, and
+    Y = alpha A X + beta Y."""
     import trilinos_amd as ta
     from oracle import epetra as oe
     if generic:
@@ -422,7 +422,7 @@ def test_spmm_march_bit_exact(comm, kind, dims, k, alpha, beta, generic, monkeyp
     nx, ny, nz = dims
     n = nx * ny * nz
     A = ta.CrsMatrix.galeri(comm, kind, nx, ny, nz)
-    assert A.spmm_kernel() == ("march" if generic or kind == "Laplace3D" else "tpl3")
+    assert A.spmm_kernel() == "march"
     gen = (lambda f, m: oe.brick3d_rows(nx, ny, nz, f, m)) if kind == "Brick3D" else \
         (lambda f, m: oe.laplace3d_rows(nx, ny, nz, f, m))
     Aor = oe.DistCrs(gen, n, 1)
@@ -470,3 +470,25 @@ def test_spmm_march_slabs_bit_exact(comm, kind, generic, kc, sz, pd, nl, dims, m
     Yd = ta.MultiVector(comm, n, k)
     A.apply(_upload(ta, comm, X), Yd)
     assert np.array_equal(Yd.download(), oe.DistCrs(gen, n, 1).apply(X))
+
+
+@pytest.mark.parametrize("perturb", ["interior", "boundary"])
+def test_spmm_march27_needs_uniform_stencil(comm, perturb):
+    """The uniform 27-point march needs one coefficient table for every pair: a Brick3D
+    operator with one coefficient changed (an interior row, or a boundary row) has templates
+    that disagree, so it keeps the lane-shared template kernel -- bit for bit either way."""
+    import trilinos_amd as ta
+    from oracle import epetra as oe
+    nx, ny, nz, k = 12, 10, 9, 4
+    n = nx * ny * nz
+    rp, gc, vv = oe.brick3d_rows(nx, ny, nz, 0, n)
+    vv = np.array(vv, dtype=np.float64)
+    row = (nz // 2 * ny + ny // 2) * nx + nx // 2 if perturb == "interior" else 1
+    vv[rp[row] + 1] = -1.25
+    A = ta.CrsMatrix(comm, n, rp, gc, vv)
+    assert A.spmm_kernel() == "tpl3"
+    Aor = oe.DistCrs(lambda f, m: (rp, gc, vv) if (f, m) == (0, n) else None, n, 1)
+    X, _ = oe.epetra_random_mv(47, n, k)
+    Yd = ta.MultiVector(comm, n, k)
+    A.apply(_upload(ta, comm, X), Yd)
+    assert np.array_equal(Yd.download(), Aor.apply(X))

@@ -206,9 +206,12 @@ def test_ranks_without_rows(kind, dims, k, P):
     np.testing.assert_allclose(rel, rel_ref, rtol=1e-6, atol=1e-13)
 
 
-@pytest.mark.parametrize("kind,dims,k,P", [("Laplace3D", (12, 10, 8), 8, 2), ("Laplace3D", (12, 10, 7), 5, 3),
-                                           ("Brick3D", (10, 8, 9), 4, 3), ("Brick3D", (14, 6, 5), 8, 4)])
-def test_distributed_spmm_march_bit_exact(kind, dims, k, P, monkeypatch):
+@pytest.mark.parametrize("kind,dims,k,P,generic", [("Laplace3D", (12, 10, 8), 8, 2, False),
+                                                   ("Laplace3D", (12, 10, 7), 5, 3, False),
+                                                   ("Brick3D", (10, 8, 9), 4, 3, True), ("Brick3D", (14, 6, 5), 8, 4, True),
+                                                   ("Brick3D", (10, 8, 9), 4, 3, False),
+                                                   ("Brick3D", (14, 6, 5), 8, 4, False)])
+def test_distributed_spmm_march_bit_exact(kind, dims, k, P, generic, monkeypatch):
     """The plane march on P ranks (loopback; the general form for Brick3D): slabs of whole
     planes take it on every rank; a
     row split in mid-plane (12 x 10 x 7 over 3 ranks, 14 x 6 x 5 over 4) puts templated pairs
@@ -216,7 +219,7 @@ def test_distributed_spmm_march_bit_exact(kind, dims, k, P, monkeypatch):
     template kernel.  Every rank bit for bit against the oracle's P-rank product."""
     import trilinos_amd as ta
     from oracle import epetra as oe
-    if kind == "Brick3D":
+    if generic:
         monkeypatch.setenv("MIGMRES_MARCH_GENERIC", "1")
     n, gen = _gen(kind, dims)
     X, _ = oe.epetra_random_mv(43, n, k)

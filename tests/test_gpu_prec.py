@@ -224,14 +224,15 @@ def test_fused_right_jacobi_under_halo_bit_identical(kind, dims, k, P, monkeypat
         assert np.array_equal(a[4], b[4])
 
 
-@pytest.mark.parametrize("kind,dims,k", [("Brick3D", (12, 10, 9), 8), ("Laplace3D", (14, 9, 8), 5),
-                                         ("Laplace3D", (12, 10, 9), 8)])
-def test_fused_right_jacobi_march_matches_template_kernels(comm, kind, dims, k, monkeypatch):
+@pytest.mark.parametrize("kind,dims,k,generic", [("Brick3D", (12, 10, 9), 8, True), ("Brick3D", (12, 10, 9), 8, False),
+                                                 ("Brick3D", (14, 7, 6), 3, False), ("Laplace3D", (14, 9, 8), 5, False),
+                                                 ("Laplace3D", (12, 10, 9), 8, False)])
+def test_fused_right_jacobi_march_matches_template_kernels(comm, kind, dims, k, generic, monkeypatch):
     """The fused right Jacobi through the plane march (the staged operand is (omega d^-1) x,
-    formed once per X pair; the 7-point specialisation for Laplace3D, the general march for
-    Brick3D) against the same solve through the template kernels (MIGMRES_NO_MARCH=1):
+    formed once per X pair; the 7-point specialisation for Laplace3D, the uniform 27-point one
+    or the general march for Brick3D) against the same solve through the template kernels (MIGMRES_NO_MARCH=1):
     bit-identical solutions, histories and counters."""
-    if kind == "Brick3D":
+    if generic:
         monkeypatch.setenv("MIGMRES_MARCH_GENERIC", "1")
     n, _ = _gen(kind, dims)
     params = {"Block Size": k, "Num Blocks": 10, "Maximum Iterations": 300, "Maximum Restarts": 30,

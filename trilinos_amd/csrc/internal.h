@@ -132,6 +132,19 @@ bool launch_spmm_march(hipStream_t s, int n_local, const unsigned char *tid, con
 bool launch_spmm_march7(hipStream_t s, int n_local, const unsigned char *tid, const unsigned long long *grp, int ntpl,
                         const MarchGeom &geom, const double *vals, int nvals, MvDesc X, MvDesc Y, double alpha,
                         double beta, const double *colscale = nullptr, int sz = 0, int pd = 2, int nl = 1);
+// The march for a UNIFORM 27-point stencil (G = 9 groups over every (plane, line) offset in
+// {-1, 0, 1}^2): one coefficient table U (slot i of group g) for every templated pair, the
+// slots a template leaves unused reading only neighbours outside the grid (march27_check).
+struct March27Coef {
+  double w[9][6];
+};
+bool launch_spmm_march27(hipStream_t s, int n_local, const unsigned char *tid, const MarchGeom &geom,
+                         const March27Coef &U, MvDesc X, MvDesc Y, double alpha, double beta,
+                         const double *colscale = nullptr, int sz = 0, int pd = 2);
+// Templated pairs with an unused slot whose neighbour lies inside the grid (umask[t]: used slots
+// of template t, bit 6 g + i); the uniform form needs none.
+int march27_check(hipStream_t s, int npairs, const unsigned char *tid, const unsigned long long *umask, int ntpl,
+                  const MarchGeom &geom);
 // Number of templated pairs that the march geometry cannot serve (a used x-neighbour half
 // across a line end, a group line outside the plane).  tbounds: per template {needs x-1 half,
 // needs x+1 half, lowest group line offset, highest}.

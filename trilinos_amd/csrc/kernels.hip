@@ -1563,6 +1563,229 @@ __global__ __launch_bounds__(256) void k_march_check(int npairs, const unsigned 
   if ((threadIdx.x & 63) == 0 && n) atomicAdd(bad, n);
 }
 
+// -------------------------------------------------------------------------------------
+// The march for the 27-point pattern (groups: every (plane, line) offset in {-1, 0, 1}^2) when
+// the stencil is UNIFORM: one coefficient table U[9][6] (the full template's) serves every
+// templated pair, and each slot a template does not use reads a neighbour outside the grid,
+// whose staged operand is zero (march27_check verifies both per pair).  Then every pair adds
+// all 54 products in k_spmm_tpl3's order -- an absent entry contributes U * 0 = +-0, which
+// leaves a running sum that starts at +0.0 unchanged -- with no per-lane coefficients or
+// masks: U sits in scalar registers / the constant cache.  Planes z - 1, z and z + 1 are read
+// from a 4-slot LDS ring (one barrier per plane); PD planes of loads in flight; one column per
+// workgroup.  Same bits as k_spmm_tpl3.
+// -------------------------------------------------------------------------------------
+template <int PD, bool CS>
+__global__ __launch_bounds__(256) void k_spmm_march27(int npairs, int n_local, const unsigned char *__restrict__ tid,
+                                                      MarchGeom mg, int txn, int tyn, int tzn, int sz, March27Coef U,
+                                                      MvDesc X, MvDesc Y, double alpha, double beta,
+                                                      const double *__restrict__ cs) {
+#pragma clang fp contract(off)
+  __shared__ __attribute__((aligned(16))) d2 ring[4 * kMarchPl];  // [4][kMarchLY][kMarchLX]
+  const int t = threadIdx.x;
+  const int ntile = txn * tyn * tzn, nwork = ntile * Y.ncols, per = (nwork + 7) >> 3;
+  const int work = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+  if (work >= nwork) return;  // uniform
+  const int c = work / ntile, tile = work % ntile;
+  const int ty = tile % tyn, tx = (tile / tyn) % txn, tz = tile / (tyn * txn);
+  const int lx = t & 63, ly = t >> 6;
+  int spos[2], soff[2];
+  bool sok[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    int line, xp;
+    if (i == 0) {
+      line = ly + 1;
+      xp = lx + 1;
+    } else if (t < 128) {
+      line = t < 64 ? 0 : kMarchLY - 1;
+      xp = lx + 1;
+    } else {
+      const int e = t - 128;
+      line = e >> 1;
+      xp = (e & 1) ? kMarchLX - 1 : 0;
+    }
+    const int gx = tx * kMarchTX + xp - 1, gy = ty * kMarchTY + line - 1;
+    sok[i] = (i == 0 || t < 140) && gx >= 0 && gx < mg.nxp && gy >= 0 && gy < mg.nyl;
+    soff[i] = sok[i] ? gy * mg.nxp + gx : 0;
+    spos[i] = line * kMarchLX + xp;
+  }
+  const int z0 = tz * sz, z1 = min(z0 + sz, mg.nz);
+  struct PlaneRegs {
+    d2 v[2];
+    d2 sc[CS ? 2 : 1];
+    int tid;
+  };
+  const double *xc = colp(X, c);
+  double *yc = colp(Y, c);
+  auto load = [&](PlaneRegs &r, int q) __attribute__((always_inline)) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const long long pr = (long long)q * mg.plane + soff[h];
+      const bool ok = sok[h] && q >= 0 && q < mg.nz && pr < npairs;
+      const long long pc = ok ? pr : 0;
+      r.v[h] = ok ? *(const d2 *)(xc + 2 * pc) : d2{0.0, 0.0};
+      if constexpr (CS) r.sc[h] = ok ? *(const d2 *)(cs + 2 * pc) : d2{0.0, 0.0};
+    }
+    const long long pr = (long long)q * mg.plane + soff[0];
+    r.tid = (sok[0] && q >= 0 && q < mg.nz && pr < npairs) ? (int)tid[pr] : 0xFF;
+  };
+  auto stage = [&](const PlaneRegs &r, int q) __attribute__((always_inline)) {
+    d2 *d = ring + (q & 3) * kMarchPl;
+    d2 o0 = r.v[0], o1 = r.v[1];
+    if constexpr (CS) {
+      o0 = r.sc[0] * r.v[0];
+      o1 = r.sc[CS ? 1 : 0] * r.v[1];
+    }
+    d[spos[0]] = o0;
+    if (t < 140) d[spos[1]] = o1;
+  };
+  PlaneRegs rb[PD];
+  int tc;
+  {
+    PlaneRegs r0;
+    load(r0, z0 - 1);
+    stage(r0, z0 - 1);
+    load(r0, z0);
+    stage(r0, z0);
+    tc = r0.tid;
+  }
+#pragma unroll
+  for (int i = 0; i < PD; ++i) load(rb[i], z0 + 1 + i);
+  for (int z = z0; z < z1; z += PD) {
+#pragma unroll
+    for (int i = 0; i < PD; ++i) {
+      const int zz = z + i;
+      if (zz < z1) {
+        stage(rb[i], zz + 1);
+        const int tzz = tc;
+        tc = rb[i].tid;
+        load(rb[i], zz + 1 + PD);
+        march_barrier();
+        if (tzz != 0xFF) {
+          double sa = 0.0, sb = 0.0;
+#pragma unroll
+          for (int a = 0; a < 3; ++a) {
+            const d2 *pl = ring + ((zz + a - 1) & 3) * kMarchPl + spos[0];
+#pragma unroll
+            for (int bq = 0; bq < 3; ++bq) {
+              const int g = 3 * a + bq;
+              const d2 *b = pl + (bq - 1) * kMarchLX;
+              const d2 x = b[0];
+              const double left = b[-1].y, right = b[1].x;
+              sa = sa + U.w[g][0] * left;
+              sa = sa + U.w[g][1] * x.x;
+              sa = sa + U.w[g][2] * x.y;
+              sb = sb + U.w[g][3] * x.x;
+              sb = sb + U.w[g][4] * x.y;
+              sb = sb + U.w[g][5] * right;
+            }
+          }
+          const long long ra = 2 * ((long long)zz * mg.plane + soff[0]);
+          double *yq = yc + ra;
+          if (beta == 0.0) {
+            if (alpha != 1.0) {
+              sa = alpha * sa;
+              sb = alpha * sb;
+            }
+          } else {
+            sa = alpha * sa + beta * yq[0];
+            if (ra + 1 < n_local) sb = alpha * sb + beta * yq[1];
+          }
+          if (ra + 1 < n_local)
+            *(d2 *)yq = d2{sa, sb};
+          else
+            yq[0] = sa;
+        }
+      }
+    }
+  }
+}
+
+bool launch_spmm_march27(hipStream_t s, int n_local, const unsigned char *tid, const MarchGeom &geom,
+                         const March27Coef &U, MvDesc X, MvDesc Y, double alpha, double beta, const double *colscale,
+                         int sz, int pd) {
+  const int npairs = (n_local + 1) / 2;
+  if (npairs <= 0 || Y.ncols <= 0) return true;
+  if (geom.nxp <= 0 || geom.nyl <= 0 || geom.plane != geom.nxp * geom.nyl ||
+      (long long)geom.nz * geom.plane < npairs)
+    return false;
+  if (sz <= 0) {
+    static int cus = 0;
+    if (!cus) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        cus = 256;
+    }
+    const long long cols = (long long)cdiv(geom.nxp, kMarchTX) * cdiv(geom.nyl, kMarchTY) * Y.ncols;
+    const long long slabs = std::max(1LL, std::min((long long)cdiv(9LL * cus, cols), (long long)cdiv(geom.nz, 4)));
+    sz = cdiv(geom.nz, slabs);
+  }
+  const int txn = cdiv(geom.nxp, kMarchTX), tyn = cdiv(geom.nyl, kMarchTY), tzn = cdiv(geom.nz, sz);
+  const int grid = 8 * ((txn * tyn * tzn * Y.ncols + 7) / 8);
+#define M27(PD)                                                                                                   \
+  if (colscale)                                                                                                   \
+    k_spmm_march27<PD, true><<<grid, 256, 0, s>>>(npairs, n_local, tid, geom, txn, tyn, tzn, sz, U, X, Y, alpha,  \
+                                                  beta, colscale);                                                \
+  else                                                                                                            \
+    k_spmm_march27<PD, false><<<grid, 256, 0, s>>>(npairs, n_local, tid, geom, txn, tyn, tzn, sz, U, X, Y, alpha, \
+                                                   beta, colscale)
+  if (pd >= 3) {
+    M27(3);
+  } else if (pd == 2) {
+    M27(2);
+  } else {
+    M27(1);
+  }
+#undef M27
+  LAUNCH_CHECK();
+  return true;
+}
+
+// Pairs for which the uniform 27-point form would differ: per templated pair, every slot its
+// template leaves unused must read a neighbour outside the grid (a staged zero).  umask[t]: the
+// template's used slots (bit 6 g + i).
+__global__ __launch_bounds__(256) void k_march27_check(int npairs, const unsigned char *__restrict__ tid,
+                                                       const unsigned long long *__restrict__ umask, MarchGeom mg,
+                                                       int *__restrict__ bad) {
+  int n = 0;
+  for (int p = blockIdx.x * 256 + threadIdx.x; p < npairs; p += gridDim.x * 256) {
+    const int t = tid[p];
+    if (t == 0xFF) continue;
+    const unsigned long long m = umask[t];
+    const int x = p % mg.nxp, y = (p / mg.nxp) % mg.nyl, z = p / mg.plane;
+    for (int g = 0; g < 9; ++g)
+      for (int i = 0; i < 6; ++i) {
+        if ((m >> (6 * g + i)) & 1ull) continue;
+        const int xq = x + (i == 0 ? -1 : i == 5 ? 1 : 0), yq = y + g % 3 - 1, zq = z + g / 3 - 1;
+        const bool inside = xq >= 0 && xq < mg.nxp && yq >= 0 && yq < mg.nyl && zq >= 0 && zq < mg.nz &&
+                            (long long)zq * mg.plane + (long long)yq * mg.nxp + xq < npairs;
+        n += inside ? 1 : 0;
+      }
+  }
+  for (int off = 32; off > 0; off >>= 1) n += __shfl_down(n, off, 64);
+  if ((threadIdx.x & 63) == 0 && n) atomicAdd(bad, n);
+}
+
+int march27_check(hipStream_t s, int npairs, const unsigned char *tid, const unsigned long long *umask, int ntpl,
+                  const MarchGeom &geom) {
+  if (npairs <= 0) return 0;
+  int *d = nullptr;
+  unsigned long long *dm = nullptr;
+  MIG_HIP(hipMalloc(&d, sizeof(int)));
+  MIG_HIP(hipMalloc(&dm, sizeof(unsigned long long) * ntpl));
+  MIG_HIP(hipMemcpyAsync(dm, umask, sizeof(unsigned long long) * ntpl, hipMemcpyHostToDevice, s));
+  MIG_HIP(hipMemsetAsync(d, 0, sizeof(int), s));
+  k_march27_check<<<std::min(cdiv(npairs, 256), 4096), 256, 0, s>>>(npairs, tid, dm, geom, d);
+  LAUNCH_CHECK();
+  int h = 0;
+  MIG_HIP(hipMemcpyAsync(&h, d, sizeof(int), hipMemcpyDeviceToHost, s));
+  MIG_HIP(hipStreamSynchronize(s));
+  hipFree(d);
+  hipFree(dm);
+  return h;
+}
+
 int march_check(hipStream_t s, int npairs, const unsigned char *tid, const int4 *tbounds, int ntpl, int nxp,
                 int nyl) {
   if (npairs <= 0) return 0;

@@ -835,25 +835,62 @@ static void setup_template_kernels(migmres_crs *A, const PairTemplates &pt) {
           }
     }
   }
-  if (!env_on("MIGMRES_NO_MARCH") && groups && (generic || seven) && mg.nxp > 0 &&
-      march_check(A->ctx->stream, pt.npairs, A->d_tpl_id, (const int4 *)mg.tb.data(), pt.ntpl, mg.nxp, mg.nyl) == 0) {
+  // the uniform 27-point form: all nine (plane, line) groups, one coefficient table (the full
+  // template's, all 54 slots used) that every template's used slots agree with bit for bit,
+  // and (checked on the device below) every unused slot reading a neighbour outside the grid
+  bool uni27 = !generic && groups && sg.G == 9 && mg.nxp > 0;
+  March27Coef U{};
+  std::vector<unsigned long long> umask((size_t)pt.ntpl, 0);
+  if (uni27) {
+    for (int g = 0; g < 9; ++g) uni27 = uni27 && mg.ga[(size_t)g] == g / 3 - 1 && mg.gb[(size_t)g] == g % 3 - 1;
+    int full = -1;
+    for (int t = 0; t < pt.ntpl && uni27; ++t) {
+      for (int g = 0; g < 9; ++g)
+        for (int i = 0; i < 6; ++i)
+          if (((sg.slots[(size_t)t * 9 + g] >> (8 * i)) & 0xFF) != kTplUnused) umask[(size_t)t] |= 1ULL << (6 * g + i);
+      if (umask[(size_t)t] == (1ULL << 54) - 1 && full < 0) full = t;
+    }
+    uni27 = uni27 && full >= 0;
+    auto value = [&](int t, int g, int i) {
+      const unsigned sl = (unsigned)(sg.slots[(size_t)t * 9 + g] >> (8 * i)) & 0xFF;
+      return sl < pt.vals.size() ? pt.vals[sl] : 0.0;
+    };
+    for (int t = 0; t < pt.ntpl && uni27; ++t)
+      for (int g = 0; g < 9; ++g)
+        for (int i = 0; i < 6; ++i) {
+          if (t == 0) U.w[g][i] = value(full, g, i);
+          const double v = value(t, g, i);
+          if (((umask[(size_t)t] >> (6 * g + i)) & 1ULL) && std::memcmp(&v, &U.w[g][i], sizeof(double)) != 0)
+            uni27 = false;
+        }
+  }
+  const bool use_march = !env_on("MIGMRES_NO_MARCH") && groups && (generic || seven || uni27) && mg.nxp > 0 &&
+                         march_check(A->ctx->stream, pt.npairs, A->d_tpl_id, (const int4 *)mg.tb.data(), pt.ntpl,
+                                     mg.nxp, mg.nyl) == 0;
+  MarchGeom geo;
+  geo.nxp = mg.nxp;
+  geo.nyl = mg.nyl;
+  geo.plane = mg.plane;
+  geo.nz = mg.nz;
+  for (int g = 0; g < sg.G && use_march; ++g) {
+    geo.ga[g] = mg.ga[(size_t)g];
+    geo.gb[g] = mg.gb[(size_t)g];
+  }
+  if (use_march && uni27 && march27_check(A->ctx->stream, pt.npairs, A->d_tpl_id, umask.data(), pt.ntpl, geo) != 0)
+    uni27 = false;
+  if (use_march && (generic || seven || uni27)) {
     upload_groups();
     A->use_march7 = seven && !generic;
-    A->march.nxp = mg.nxp;
-    A->march.nyl = mg.nyl;
-    A->march.plane = mg.plane;
-    A->march.nz = mg.nz;
-    for (int g = 0; g < sg.G; ++g) {
-      A->march.ga[g] = mg.ga[(size_t)g];
-      A->march.gb[g] = mg.gb[(size_t)g];
-    }
+    A->use_march27 = uni27;
+    A->march27_coef = U;
+    A->march = geo;
     A->use_march = true;
     const char *kc = std::getenv("MIGMRES_MARCH_KC");
     A->march_kc = kc ? std::atoi(kc) : 2;
     const char *sz = std::getenv("MIGMRES_MARCH_SZ");
     A->march_sz = sz ? std::atoi(sz) : 0;
     const char *pd = std::getenv("MIGMRES_MARCH_PD");
-    A->march_pd = pd ? std::atoi(pd) : (A->use_march7 ? 3 : 1);
+    A->march_pd = pd ? std::atoi(pd) : (A->use_march7 ? 3 : A->use_march27 ? 2 : 1);
     const char *nl = std::getenv("MIGMRES_MARCH_NL");
     A->march_nl = nl ? std::atoi(nl) : 1;
     return;
@@ -1233,7 +1270,9 @@ static void crs_apply_impl(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, d
   if (A.use_tpl) {
     // templated pairs read no ghost column: they run while the halo is in flight, then the
     // pairs that do read one go to the fallback kernel
-    bool done = A.use_march7 ? launch_spmm_march7(c->stream, A.n_local, A.d_tpl_id, A.d_tpl3_grp, A.tpl_ntpl,
+    bool done = A.use_march27 ? launch_spmm_march27(c->stream, A.n_local, A.d_tpl_id, A.march, A.march27_coef,
+                                                    X.desc(), Y.desc(), alpha, beta, cs.own, A.march_sz, A.march_pd)
+                : A.use_march7 ? launch_spmm_march7(c->stream, A.n_local, A.d_tpl_id, A.d_tpl3_grp, A.tpl_ntpl,
                                                   A.march, A.d_tpl_val, A.tpl_nvals, X.desc(), Y.desc(), alpha,
                                                   beta, cs.own, A.march_sz, A.march_pd, A.march_nl)
                 : A.use_march && launch_spmm_march(c->stream, A.n_local, A.d_tpl_id, A.d_tpl3_grp, A.tpl_ntpl,
