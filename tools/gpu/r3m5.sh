@@ -6,6 +6,7 @@ MIGMRES_NO_MARCH=1 step 120 ts_bk_tpl3_$P.log python tools/time_spmm.py Brick3D 
 for pd in 1 2 3; do
   MIGMRES_MARCH_PD=$pd step 120 ts_bk_pd${pd}_$P.log python tools/time_spmm.py Brick3D 256 8
 done
+MIGMRES_MARCH27_TABLE=1 step 120 ts_bk_table_$P.log python tools/time_spmm.py Brick3D 256 8
 step 120 ts_bk384_$P.log python tools/time_spmm.py Brick3D 384 8
 MIGMRES_NO_MARCH=1 step 120 ts_bk384_tpl3_$P.log python tools/time_spmm.py Brick3D 384 8
 step 300 bench_bj_$P.json python bench.py --no-cpu-baseline --matrix Brick3D --prec right

@@ -137,6 +137,11 @@ bool launch_spmm_march7(hipStream_t s, int n_local, const unsigned char *tid, co
 // slots a template leaves unused reading only neighbours outside the grid (march27_check).
 struct March27Coef {
   double w[9][6];
+  // two_valued: every w[g][i] is v2[(sel >> (6 g + i)) & 1] (Galeri's stencils: centre and
+  // neighbour value), so the kernel keeps 2 values instead of 54 in scalar registers
+  int two_valued = 0;
+  double v2[2] = {0.0, 0.0};
+  unsigned long long sel = 0;
 };
 bool launch_spmm_march27(hipStream_t s, int n_local, const unsigned char *tid, const MarchGeom &geom,
                          const March27Coef &U, MvDesc X, MvDesc Y, double alpha, double beta,

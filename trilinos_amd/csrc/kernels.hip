@@ -1574,7 +1574,7 @@ __global__ __launch_bounds__(256) void k_march_check(int npairs, const unsigned 
 // from a 4-slot LDS ring (one barrier per plane); PD planes of loads in flight; one column per
 // workgroup.  Same bits as k_spmm_tpl3.
 // -------------------------------------------------------------------------------------
-template <int PD, bool CS>
+template <int PD, bool CS, bool TWO>
 __global__ __launch_bounds__(256) void k_spmm_march27(int npairs, int n_local, const unsigned char *__restrict__ tid,
                                                       MarchGeom mg, int txn, int tyn, int tzn, int sz, March27Coef U,
                                                       MvDesc X, MvDesc Y, double alpha, double beta,
@@ -1672,12 +1672,15 @@ __global__ __launch_bounds__(256) void k_spmm_march27(int npairs, int n_local, c
               const d2 *b = pl + (bq - 1) * kMarchLX;
               const d2 x = b[0];
               const double left = b[-1].y, right = b[1].x;
-              sa = sa + U.w[g][0] * left;
-              sa = sa + U.w[g][1] * x.x;
-              sa = sa + U.w[g][2] * x.y;
-              sb = sb + U.w[g][3] * x.x;
-              sb = sb + U.w[g][4] * x.y;
-              sb = sb + U.w[g][5] * right;
+              auto w = [&](int i) __attribute__((always_inline)) {
+                return TWO ? ((U.sel >> (6 * g + i)) & 1ULL ? U.v2[1] : U.v2[0]) : U.w[g][i];
+              };
+              sa = sa + w(0) * left;
+              sa = sa + w(1) * x.x;
+              sa = sa + w(2) * x.y;
+              sb = sb + w(3) * x.x;
+              sb = sb + w(4) * x.y;
+              sb = sb + w(5) * right;
             }
           }
           const long long ra = 2 * ((long long)zz * mg.plane + soff[0]);
@@ -1723,21 +1726,28 @@ bool launch_spmm_march27(hipStream_t s, int n_local, const unsigned char *tid, c
   }
   const int txn = cdiv(geom.nxp, kMarchTX), tyn = cdiv(geom.nyl, kMarchTY), tzn = cdiv(geom.nz, sz);
   const int grid = 8 * ((txn * tyn * tzn * Y.ncols + 7) / 8);
-#define M27(PD)                                                                                                   \
+#define M27T(PD, TWO)                                                                                             \
   if (colscale)                                                                                                   \
-    k_spmm_march27<PD, true><<<grid, 256, 0, s>>>(npairs, n_local, tid, geom, txn, tyn, tzn, sz, U, X, Y, alpha,  \
-                                                  beta, colscale);                                                \
+    k_spmm_march27<PD, true, TWO><<<grid, 256, 0, s>>>(npairs, n_local, tid, geom, txn, tyn, tzn, sz, U, X, Y,    \
+                                                       alpha, beta, colscale);                                    \
   else                                                                                                            \
-    k_spmm_march27<PD, false><<<grid, 256, 0, s>>>(npairs, n_local, tid, geom, txn, tyn, tzn, sz, U, X, Y, alpha, \
-                                                   beta, colscale)
+    k_spmm_march27<PD, false, TWO><<<grid, 256, 0, s>>>(npairs, n_local, tid, geom, txn, tyn, tzn, sz, U, X, Y,   \
+                                                        alpha, beta, colscale)
+#define M27(PD)          \
+  if (U.two_valued) {    \
+    M27T(PD, true);      \
+  } else {               \
+    M27T(PD, false);     \
+  }
   if (pd >= 3) {
-    M27(3);
+    M27(3)
   } else if (pd == 2) {
-    M27(2);
+    M27(2)
   } else {
-    M27(1);
+    M27(1)
   }
 #undef M27
+#undef M27T
   LAUNCH_CHECK();
   return true;
 }

@@ -864,6 +864,21 @@ static void setup_template_kernels(migmres_crs *A, const PairTemplates &pt) {
             uni27 = false;
         }
   }
+  if (uni27 && !env_on("MIGMRES_MARCH27_TABLE")) {  // at most two distinct values: select, not a 54-entry table
+    int nv = 0;
+    for (int g = 0; g < 9; ++g)
+      for (int i = 0; i < 6; ++i) {
+        const double v = U.w[g][i];
+        int which = -1;
+        for (int q = 0; q < nv; ++q)
+          if (std::memcmp(&v, &U.v2[q], sizeof(double)) == 0) which = q;
+        if (which < 0 && nv < 2) U.v2[which = nv++] = v;
+        if (which < 0) nv = 3;
+        if (which == 1) U.sel |= 1ULL << (6 * g + i);
+      }
+    U.two_valued = nv <= 2 ? 1 : 0;
+    if (!U.two_valued) U.sel = 0;
+  }
   const bool use_march = !env_on("MIGMRES_NO_MARCH") && groups && (generic || seven || uni27) && mg.nxp > 0 &&
                          march_check(A->ctx->stream, pt.npairs, A->d_tpl_id, (const int4 *)mg.tb.data(), pt.ntpl,
                                      mg.nxp, mg.nyl) == 0;
