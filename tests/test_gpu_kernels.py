@@ -492,3 +492,29 @@ def test_spmm_march27_needs_uniform_stencil(comm, perturb):
     Yd = ta.MultiVector(comm, n, k)
     A.apply(_upload(ta, comm, X), Yd)
     assert np.array_equal(Yd.download(), Aor.apply(X))
+
+
+@pytest.mark.parametrize("mode", ["uniform", "lane", "perturbed"])
+def test_spmm_march7_coefficient_forms(comm, mode, monkeypatch):
+    """The 7-point march keeps no per-lane coefficients when the stencil is uniform (one table,
+    absent entries reading out-of-grid zeros); with per-lane coefficients forced
+    (MIGMRES_MARCH7_LANE_COEF=1) or a coefficient perturbed in one interior row (the templates
+    then disagree), it reads each lane's template coefficients: bit for bit either way."""
+    import trilinos_amd as ta
+    from oracle import epetra as oe
+    nx, ny, nz, k = 14, 9, 8, 3
+    n = nx * ny * nz
+    rp, gc, vv = oe.laplace3d_rows(nx, ny, nz, 0, n)
+    vv = np.array(vv, dtype=np.float64)
+    if mode == "lane":
+        monkeypatch.setenv("MIGMRES_MARCH7_LANE_COEF", "1")
+    if mode == "perturbed":
+        row = (nz // 2 * ny + ny // 2) * nx + nx // 2
+        vv[rp[row] + 2] = -0.75
+    A = ta.CrsMatrix(comm, n, rp, gc, vv)
+    assert A.spmm_kernel() == "march"
+    Aor = oe.DistCrs(lambda f, m: (rp, gc, vv), n, 1)
+    X, _ = oe.epetra_random_mv(53, n, k)
+    Yd = ta.MultiVector(comm, n, k)
+    A.apply(_upload(ta, comm, X), Yd)
+    assert np.array_equal(Yd.download(), Aor.apply(X))

@@ -7,6 +7,8 @@ for kind in Laplace3D Brick3D; do
   step 120 ts_${kind}_march_$P.log python tools/time_spmm.py $kind 256 8
   MIGMRES_NO_MARCH=1 step 120 ts_${kind}_tpl_$P.log python tools/time_spmm.py $kind 256 8
   MIGMRES_MARCH_KC=1 step 120 ts_${kind}_kc1_$P.log python tools/time_spmm.py $kind 256 8
+  MIGMRES_MARCH_PD=2 step 120 ts_${kind}_pd2_$P.log python tools/time_spmm.py $kind 256 8
+  MIGMRES_MARCH_PD=2 MIGMRES_MARCH_KC=1 step 120 ts_${kind}_pd2kc1_$P.log python tools/time_spmm.py $kind 256 8
 done
 step 300 bench_256_$P.json python bench.py --no-cpu-baseline
 MIGMRES_NO_MARCH=1 step 300 bench_256_nomarch_$P.json python bench.py --no-cpu-baseline

@@ -27,6 +27,9 @@ KMAP = {"k_gemm_tn": ("gemm_tn", True), "k_gemm_nn": ("gemm_nn", True),
         "k_spmm": ("spmm", False), "k_spmm_pair": ("spmm", False),
         # template SpMM: X pairs are 16-B/lane loads (the 1-B template ids are 0.4 % of the bytes)
         "k_spmm_tplr": ("spmm", True), "k_spmm_tpl": ("spmm", True), "k_spmm_sell": ("spmm", False),
+        # lane-shared template and plane-march SpMM: X pairs as 16-B/lane loads
+        "k_spmm_tpl3": ("spmm", True), "k_spmm_march": ("spmm", True), "k_spmm_march7": ("spmm", True),
+        "k_spmm_march27": ("spmm", True),
         "k_fb_a": ("findbasis", True), "k_fb_a01": ("findbasis", True), "k_fb_b2": ("findbasis", True),
         "k_fb_ca": ("findbasis", True), "k_gemm_nn_gram": ("gemm_nn_dot", True),
         "k_fbg_gram": ("findbasis", True), "k_fbg_a": ("findbasis", True), "k_fbg_b": ("findbasis", True),

@@ -125,13 +125,6 @@ struct MarchGeom {
 bool launch_spmm_march(hipStream_t s, int n_local, const unsigned char *tid, const unsigned long long *grp, int ntpl,
                        int G, const MarchGeom &geom, const double *vals, int nvals, MvDesc X, MvDesc Y, double alpha,
                        double beta, const double *colscale = nullptr, int kcmax = 2, int sz = 0, int pd = 1);
-// The march for the 7-point pattern (G = 5: groups (z - 1), (y - 1), x line, (y + 1), (z + 1)
-// with neighbour halves only on the x line): coefficients in registers, only plane z staged,
-// the (z +- 1) centres from the lane's own loads; pd planes of loads in flight (1..3), nl lines
-// per thread (1, 2: tiles of 4 nl lines).
-bool launch_spmm_march7(hipStream_t s, int n_local, const unsigned char *tid, const unsigned long long *grp, int ntpl,
-                        const MarchGeom &geom, const double *vals, int nvals, MvDesc X, MvDesc Y, double alpha,
-                        double beta, const double *colscale = nullptr, int sz = 0, int pd = 2, int nl = 1);
 // The march for a UNIFORM 27-point stencil (G = 9 groups over every (plane, line) offset in
 // {-1, 0, 1}^2): one coefficient table U (slot i of group g) for every templated pair, the
 // slots a template leaves unused reading only neighbours outside the grid (march27_check).
@@ -142,14 +135,26 @@ struct March27Coef {
   int two_valued = 0;
   double v2[2] = {0.0, 0.0};
   unsigned long long sel = 0;
+  unsigned long long used = 0;  // slots the full template uses (the others are skipped by every pair)
 };
+// The march for the 7-point pattern (G = 5: groups (z - 1), (y - 1), x line, (y + 1), (z + 1)
+// with neighbour halves only on the x line): coefficients in registers, only plane z staged,
+// the (z +- 1) centres from the lane's own loads; pd planes of loads in flight (1..3), nl lines
+// per thread (1, 2: tiles of 4 nl lines).
+// uni (optional): the stencil is uniform in the sense of march27_check over the five groups --
+// one coefficient table for every pair, absent entries reading out-of-grid zeros -- so the
+// kernel keeps no per-lane coefficients or masks.
+bool launch_spmm_march7(hipStream_t s, int n_local, const unsigned char *tid, const unsigned long long *grp, int ntpl,
+                        const MarchGeom &geom, const double *vals, int nvals, MvDesc X, MvDesc Y, double alpha,
+                        double beta, const double *colscale = nullptr, int sz = 0, int pd = 2, int nl = 1,
+                        const struct March27Coef *uni = nullptr);
 bool launch_spmm_march27(hipStream_t s, int n_local, const unsigned char *tid, const MarchGeom &geom,
                          const March27Coef &U, MvDesc X, MvDesc Y, double alpha, double beta,
                          const double *colscale = nullptr, int sz = 0, int pd = 2);
 // Templated pairs with an unused slot whose neighbour lies inside the grid (umask[t]: used slots
 // of template t, bit 6 g + i); the uniform form needs none.
 int march27_check(hipStream_t s, int npairs, const unsigned char *tid, const unsigned long long *umask, int ntpl,
-                  const MarchGeom &geom);
+                  const MarchGeom &geom, int G = 9, unsigned long long skip = 0);
 // Number of templated pairs that the march geometry cannot serve (a used x-neighbour half
 // across a line end, a group line outside the plane).  tbounds: per template {needs x-1 half,
 // needs x+1 half, lowest group line offset, highest}.

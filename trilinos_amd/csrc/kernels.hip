@@ -1309,12 +1309,13 @@ bool launch_spmm_march(hipStream_t s, int n_local, const unsigned char *tid, con
 // template -- the (z +- 1), (y +- 1) groups' neighbour halves -- would add +0.0, which leaves a
 // running sum that starts at +0.0 unchanged): the same bits.
 // -------------------------------------------------------------------------------------
-template <int PD, bool CS, int NL>
+template <int PD, bool CS, int NL, bool UNI>
 __global__ __launch_bounds__(256) void k_spmm_march7(int npairs, int n_local, const unsigned char *__restrict__ tid,
                                                      const unsigned long long *__restrict__ grp, int ntpl,
                                                      MarchGeom mg, int txn, int tyn, int tzn, int sz,
                                                      const double *__restrict__ vals, int nvals, MvDesc X, MvDesc Y,
-                                                     double alpha, double beta, const double *__restrict__ cs) {
+                                                     double alpha, double beta, const double *__restrict__ cs,
+                                                     March27Coef U) {
 #pragma clang fp contract(off)
   // NL lines per thread: tile of 64 pairs x 4 NL lines, staged with a one-pair / one-line halo
   constexpr int TY = 4 * NL, LY = TY + 2, PL = LY * kMarchLX, NH = 128 + 2 * LY, NS = NL + 1;
@@ -1444,7 +1445,7 @@ __global__ __launch_bounds__(256) void k_spmm_march7(int npairs, int n_local, co
         for (int l = 0; l < NL; ++l) {
           const int tl = tzz[l];
           if (tl != 0xFF) {
-            if (tl != tcoef) {  // the lines of a tile share a template away from the grid edges
+            if (!UNI && tl != tcoef) {  // the lines of a tile share a template away from the grid edges
 #pragma unroll
               for (int r = 0; r < 30; ++r) w[r] = s_coef[tl * 30 + r];
               msk = s_mask[tl];
@@ -1455,15 +1456,34 @@ __global__ __launch_bounds__(256) void k_spmm_march7(int npairs, int n_local, co
             const double left = b[-1].y, right = b[1].x;
             const d2 ctr[5] = {om[l], ym, oz[l], yp, op[l]};
             double sa = 0.0, sb = 0.0;
+            if constexpr (UNI) {
+              // uniform stencil: every pair adds the full template's products (absent entries
+              // read out-of-grid zeros); slots the full template does not use are skipped
+              auto uw = [&](int g, int i) __attribute__((always_inline)) {
+                return U.two_valued ? ((U.sel >> (6 * g + i)) & 1ULL ? U.v2[1] : U.v2[0]) : U.w[g][i];
+              };
+              auto on = [&](int g, int i) __attribute__((always_inline)) { return ((U.used >> (6 * g + i)) & 1ULL) != 0; };
 #pragma unroll
-            for (int g = 0; g < 5; ++g) {
-              const d2 x = ctr[g];
-              if (g == 2) sa = sa + ((msk >> 12) & 1u ? w[12] * left : 0.0);
-              sa = sa + ((msk >> (6 * g + 1)) & 1u ? w[6 * g + 1] * x.x : 0.0);
-              sa = sa + ((msk >> (6 * g + 2)) & 1u ? w[6 * g + 2] * x.y : 0.0);
-              sb = sb + ((msk >> (6 * g + 3)) & 1u ? w[6 * g + 3] * x.x : 0.0);
-              sb = sb + ((msk >> (6 * g + 4)) & 1u ? w[6 * g + 4] * x.y : 0.0);
-              if (g == 2) sb = sb + ((msk >> 17) & 1u ? w[17] * right : 0.0);
+              for (int g = 0; g < 5; ++g) {
+                const d2 x = ctr[g];
+                if (g == 2 && on(2, 0)) sa = sa + uw(2, 0) * left;
+                if (on(g, 1)) sa = sa + uw(g, 1) * x.x;
+                if (on(g, 2)) sa = sa + uw(g, 2) * x.y;
+                if (on(g, 3)) sb = sb + uw(g, 3) * x.x;
+                if (on(g, 4)) sb = sb + uw(g, 4) * x.y;
+                if (g == 2 && on(2, 5)) sb = sb + uw(2, 5) * right;
+              }
+            } else {
+#pragma unroll
+              for (int g = 0; g < 5; ++g) {
+                const d2 x = ctr[g];
+                if (g == 2) sa = sa + ((msk >> 12) & 1u ? w[12] * left : 0.0);
+                sa = sa + ((msk >> (6 * g + 1)) & 1u ? w[6 * g + 1] * x.x : 0.0);
+                sa = sa + ((msk >> (6 * g + 2)) & 1u ? w[6 * g + 2] * x.y : 0.0);
+                sb = sb + ((msk >> (6 * g + 3)) & 1u ? w[6 * g + 3] * x.x : 0.0);
+                sb = sb + ((msk >> (6 * g + 4)) & 1u ? w[6 * g + 4] * x.y : 0.0);
+                if (g == 2) sb = sb + ((msk >> 17) & 1u ? w[17] * right : 0.0);
+              }
             }
             const long long ra = 2 * ((long long)zz * mg.plane + soff[l]);
             double *yq = yc + ra;
@@ -1492,7 +1512,7 @@ __global__ __launch_bounds__(256) void k_spmm_march7(int npairs, int n_local, co
 
 bool launch_spmm_march7(hipStream_t s, int n_local, const unsigned char *tid, const unsigned long long *grp, int ntpl,
                         const MarchGeom &geom, const double *vals, int nvals, MvDesc X, MvDesc Y, double alpha,
-                        double beta, const double *colscale, int sz, int pd, int nl) {
+                        double beta, const double *colscale, int sz, int pd, int nl, const March27Coef *uni) {
   const int npairs = (n_local + 1) / 2;
   if (npairs <= 0 || Y.ncols <= 0) return true;
   if (geom.nxp <= 0 || geom.nyl <= 0 || geom.plane != geom.nxp * geom.nyl ||
@@ -1519,31 +1539,39 @@ bool launch_spmm_march7(hipStream_t s, int n_local, const unsigned char *tid, co
   const size_t lds =
       sizeof(d2) * 3 * (TY + 2) * kMarchLX + sizeof(double) * 30 * ntpl + sizeof(unsigned) * ntpl;
   const int grid = 8 * ((ntile + 7) / 8);
-#define M7(PD, NL)                                                                                                    \
+  const March27Coef U = uni ? *uni : March27Coef{};
+#define M7U(PD, NL, UNI)                                                                                              \
   if (colscale)                                                                                                       \
-    k_spmm_march7<PD, true, NL><<<grid, 256, lds, s>>>(npairs, n_local, tid, grp, ntpl, geom, txn, tyn, tzn, sz,     \
-                                                       vals, nvals, X, Y, alpha, beta, colscale);                    \
+    k_spmm_march7<PD, true, NL, UNI><<<grid, 256, lds, s>>>(npairs, n_local, tid, grp, ntpl, geom, txn, tyn, tzn,    \
+                                                            sz, vals, nvals, X, Y, alpha, beta, colscale, U);         \
   else                                                                                                                \
-    k_spmm_march7<PD, false, NL><<<grid, 256, lds, s>>>(npairs, n_local, tid, grp, ntpl, geom, txn, tyn, tzn, sz,    \
-                                                        vals, nvals, X, Y, alpha, beta, colscale)
+    k_spmm_march7<PD, false, NL, UNI><<<grid, 256, lds, s>>>(npairs, n_local, tid, grp, ntpl, geom, txn, tyn, tzn,   \
+                                                             sz, vals, nvals, X, Y, alpha, beta, colscale, U)
+#define M7(PD, NL)     \
+  if (uni) {           \
+    M7U(PD, NL, true); \
+  } else {             \
+    M7U(PD, NL, false);\
+  }
   if (nl == 2) {
     if (pd >= 3) {
-      M7(3, 2);
+      M7(3, 2)
     } else if (pd == 2) {
-      M7(2, 2);
+      M7(2, 2)
     } else {
-      M7(1, 2);
+      M7(1, 2)
     }
   } else {
     if (pd >= 3) {
-      M7(3, 1);
+      M7(3, 1)
     } else if (pd == 2) {
-      M7(2, 1);
+      M7(2, 1)
     } else {
-      M7(1, 1);
+      M7(1, 1)
     }
   }
 #undef M7
+#undef M7U
   LAUNCH_CHECK();
   return true;
 }
@@ -1757,17 +1785,17 @@ bool launch_spmm_march27(hipStream_t s, int n_local, const unsigned char *tid, c
 // template's used slots (bit 6 g + i).
 __global__ __launch_bounds__(256) void k_march27_check(int npairs, const unsigned char *__restrict__ tid,
                                                        const unsigned long long *__restrict__ umask, MarchGeom mg,
-                                                       int *__restrict__ bad) {
+                                                       int G, unsigned long long skip, int *__restrict__ bad) {
   int n = 0;
   for (int p = blockIdx.x * 256 + threadIdx.x; p < npairs; p += gridDim.x * 256) {
     const int t = tid[p];
     if (t == 0xFF) continue;
-    const unsigned long long m = umask[t];
+    const unsigned long long m = umask[t] | skip;
     const int x = p % mg.nxp, y = (p / mg.nxp) % mg.nyl, z = p / mg.plane;
-    for (int g = 0; g < 9; ++g)
+    for (int g = 0; g < G; ++g)
       for (int i = 0; i < 6; ++i) {
         if ((m >> (6 * g + i)) & 1ull) continue;
-        const int xq = x + (i == 0 ? -1 : i == 5 ? 1 : 0), yq = y + g % 3 - 1, zq = z + g / 3 - 1;
+        const int xq = x + (i == 0 ? -1 : i == 5 ? 1 : 0), yq = y + mg.gb[g], zq = z + mg.ga[g];
         const bool inside = xq >= 0 && xq < mg.nxp && yq >= 0 && yq < mg.nyl && zq >= 0 && zq < mg.nz &&
                             (long long)zq * mg.plane + (long long)yq * mg.nxp + xq < npairs;
         n += inside ? 1 : 0;
@@ -1778,7 +1806,7 @@ __global__ __launch_bounds__(256) void k_march27_check(int npairs, const unsigne
 }
 
 int march27_check(hipStream_t s, int npairs, const unsigned char *tid, const unsigned long long *umask, int ntpl,
-                  const MarchGeom &geom) {
+                  const MarchGeom &geom, int G, unsigned long long skip) {
   if (npairs <= 0) return 0;
   int *d = nullptr;
   unsigned long long *dm = nullptr;
@@ -1786,7 +1814,7 @@ int march27_check(hipStream_t s, int npairs, const unsigned char *tid, const uns
   MIG_HIP(hipMalloc(&dm, sizeof(unsigned long long) * ntpl));
   MIG_HIP(hipMemcpyAsync(dm, umask, sizeof(unsigned long long) * ntpl, hipMemcpyHostToDevice, s));
   MIG_HIP(hipMemsetAsync(d, 0, sizeof(int), s));
-  k_march27_check<<<std::min(cdiv(npairs, 256), 4096), 256, 0, s>>>(npairs, tid, dm, geom, d);
+  k_march27_check<<<std::min(cdiv(npairs, 256), 4096), 256, 0, s>>>(npairs, tid, dm, geom, G, skip, d);
   LAUNCH_CHECK();
   int h = 0;
   MIG_HIP(hipMemcpyAsync(&h, d, sizeof(int), hipMemcpyDeviceToHost, s));

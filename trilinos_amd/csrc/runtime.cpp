@@ -835,39 +835,51 @@ static void setup_template_kernels(migmres_crs *A, const PairTemplates &pt) {
           }
     }
   }
-  // the uniform 27-point form: all nine (plane, line) groups, one coefficient table (the full
-  // template's, all 54 slots used) that every template's used slots agree with bit for bit,
-  // and (checked on the device below) every unused slot reading a neighbour outside the grid
-  bool uni27 = !generic && groups && sg.G == 9 && mg.nxp > 0;
+  // Uniform stencil forms (the 27-point march, and the 7-point march without per-lane
+  // coefficients): a full template -- one whose used slots contain every template's -- whose
+  // values every template's used slots agree with bit for bit; every slot a template leaves
+  // unused (of those the full template uses) must read a neighbour outside the grid, which
+  // march27_check verifies on the device below.  The 27-point form also needs all 54 slots used.
+  const int Gu = sg.G;
   March27Coef U{};
   std::vector<unsigned long long> umask((size_t)pt.ntpl, 0);
-  if (uni27) {
-    for (int g = 0; g < 9; ++g) uni27 = uni27 && mg.ga[(size_t)g] == g / 3 - 1 && mg.gb[(size_t)g] == g % 3 - 1;
-    int full = -1;
-    for (int t = 0; t < pt.ntpl && uni27; ++t) {
-      for (int g = 0; g < 9; ++g)
-        for (int i = 0; i < 6; ++i)
-          if (((sg.slots[(size_t)t * 9 + g] >> (8 * i)) & 0xFF) != kTplUnused) umask[(size_t)t] |= 1ULL << (6 * g + i);
-      if (umask[(size_t)t] == (1ULL << 54) - 1 && full < 0) full = t;
-    }
-    uni27 = uni27 && full >= 0;
+  bool uniform = !generic && groups && (Gu == 9 || Gu == 5) && mg.nxp > 0;
+  if (uniform && Gu == 9)
+    for (int g = 0; g < 9; ++g) uniform = uniform && mg.ga[(size_t)g] == g / 3 - 1 && mg.gb[(size_t)g] == g % 3 - 1;
+  if (uniform && Gu == 5) uniform = seven;
+  int full = -1;
+  for (int t = 0; t < pt.ntpl && uniform; ++t) {
+    for (int g = 0; g < Gu; ++g)
+      for (int i = 0; i < 6; ++i)
+        if (((sg.slots[(size_t)t * Gu + g] >> (8 * i)) & 0xFF) != kTplUnused) umask[(size_t)t] |= 1ULL << (6 * g + i);
+    if (full < 0 || __builtin_popcountll(umask[(size_t)t]) > __builtin_popcountll(umask[(size_t)full])) full = t;
+  }
+  uniform = uniform && full >= 0 && (Gu != 9 || umask[(size_t)full] == (1ULL << 54) - 1);
+  if (uniform) {
     auto value = [&](int t, int g, int i) {
-      const unsigned sl = (unsigned)(sg.slots[(size_t)t * 9 + g] >> (8 * i)) & 0xFF;
+      const unsigned sl = (unsigned)(sg.slots[(size_t)t * Gu + g] >> (8 * i)) & 0xFF;
       return sl < pt.vals.size() ? pt.vals[sl] : 0.0;
     };
-    for (int t = 0; t < pt.ntpl && uni27; ++t)
-      for (int g = 0; g < 9; ++g)
+    U.used = umask[(size_t)full];
+    for (int g = 0; g < Gu; ++g)
+      for (int i = 0; i < 6; ++i) U.w[g][i] = value(full, g, i);
+    for (int t = 0; t < pt.ntpl && uniform; ++t) {
+      if ((umask[(size_t)t] & ~U.used) != 0) uniform = false;
+      for (int g = 0; g < Gu; ++g)
         for (int i = 0; i < 6; ++i) {
-          if (t == 0) U.w[g][i] = value(full, g, i);
           const double v = value(t, g, i);
           if (((umask[(size_t)t] >> (6 * g + i)) & 1ULL) && std::memcmp(&v, &U.w[g][i], sizeof(double)) != 0)
-            uni27 = false;
+            uniform = false;
         }
+    }
   }
-  if (uni27 && !env_on("MIGMRES_MARCH27_TABLE")) {  // at most two distinct values: select, not a 54-entry table
+  bool uni27 = uniform && Gu == 9;
+  bool uni7 = uniform && Gu == 5 && !env_on("MIGMRES_MARCH7_LANE_COEF");
+  if (uniform && !env_on("MIGMRES_MARCH27_TABLE")) {  // at most two distinct values: select, not a table
     int nv = 0;
-    for (int g = 0; g < 9; ++g)
+    for (int g = 0; g < Gu; ++g)
       for (int i = 0; i < 6; ++i) {
+        if (!((U.used >> (6 * g + i)) & 1ULL)) continue;
         const double v = U.w[g][i];
         int which = -1;
         for (int q = 0; q < nv; ++q)
@@ -891,12 +903,15 @@ static void setup_template_kernels(migmres_crs *A, const PairTemplates &pt) {
     geo.ga[g] = mg.ga[(size_t)g];
     geo.gb[g] = mg.gb[(size_t)g];
   }
-  if (use_march && uni27 && march27_check(A->ctx->stream, pt.npairs, A->d_tpl_id, umask.data(), pt.ntpl, geo) != 0)
-    uni27 = false;
+  if (use_march && (uni27 || uni7) &&
+      march27_check(A->ctx->stream, pt.npairs, A->d_tpl_id, umask.data(), pt.ntpl, geo, Gu,
+                    ~U.used & ((1ULL << (6 * Gu)) - 1)) != 0)
+    uni27 = uni7 = false;
   if (use_march && (generic || seven || uni27)) {
     upload_groups();
     A->use_march7 = seven && !generic;
     A->use_march27 = uni27;
+    A->march_uni7 = uni7 && A->use_march7;
     A->march27_coef = U;
     A->march = geo;
     A->use_march = true;
@@ -905,7 +920,7 @@ static void setup_template_kernels(migmres_crs *A, const PairTemplates &pt) {
     const char *sz = std::getenv("MIGMRES_MARCH_SZ");
     A->march_sz = sz ? std::atoi(sz) : 0;
     const char *pd = std::getenv("MIGMRES_MARCH_PD");
-    A->march_pd = pd ? std::atoi(pd) : (A->use_march7 ? 3 : A->use_march27 ? 2 : 1);
+    A->march_pd = pd ? std::atoi(pd) : (A->use_march7 ? (A->march_uni7 ? 2 : 3) : A->use_march27 ? 2 : 1);
     const char *nl = std::getenv("MIGMRES_MARCH_NL");
     A->march_nl = nl ? std::atoi(nl) : 1;
     return;
@@ -1289,7 +1304,8 @@ static void crs_apply_impl(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, d
                                                     X.desc(), Y.desc(), alpha, beta, cs.own, A.march_sz, A.march_pd)
                 : A.use_march7 ? launch_spmm_march7(c->stream, A.n_local, A.d_tpl_id, A.d_tpl3_grp, A.tpl_ntpl,
                                                   A.march, A.d_tpl_val, A.tpl_nvals, X.desc(), Y.desc(), alpha,
-                                                  beta, cs.own, A.march_sz, A.march_pd, A.march_nl)
+                                                  beta, cs.own, A.march_sz, A.march_pd, A.march_nl,
+                                                  A.march_uni7 ? &A.march27_coef : nullptr)
                 : A.use_march && launch_spmm_march(c->stream, A.n_local, A.d_tpl_id, A.d_tpl3_grp, A.tpl_ntpl,
                                                    A.tpl3_G, A.march, A.d_tpl_val, A.tpl_nvals, X.desc(), Y.desc(),
                                                    alpha, beta, cs.own, A.march_kc, A.march_sz, A.march_pd);

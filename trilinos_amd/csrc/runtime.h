@@ -179,6 +179,7 @@ struct migmres_crs {
   bool use_march = false;
   bool use_march7 = false;  // the 7-point specialisation (k_spmm_march7)
   bool use_march27 = false;  // the uniform 27-point specialisation (k_spmm_march27)
+  bool march_uni7 = false;   // k_spmm_march7 with the uniform coefficient table (no per-lane coefficients)
   migmres::March27Coef march27_coef{};
   int march_kc = 2, march_sz = 0, march_pd = 1, march_nl = 1;  // columns per staged plane, planes per slab (0: auto), planes prefetched
   int tpl_slabs = 0, tpl_kc = 8;
