@@ -267,7 +267,7 @@ __global__ void k_b3_fill(const int *rowptr, const int *cols, const double *vals
     const long long slot = off[c] + 64LL * s;
     bcol[slot + lane] = cols[rowptr[3 * b] + 3 * s];
     for (int r = 0; r < 3; ++r)
-      for (int e = 0; e < 3; ++e) bval[9 * slot + 64 * (3 * r + e) + lane] = vals[rowptr[3 * b + r] + 3 * s + e];
+      for (int e = 0; e < 3; ++e) bval[bsr3_val_index(slot, 3 * r + e, lane)] = vals[rowptr[3 * b + r] + 3 * s + e];
   }
 }
 

@@ -318,7 +318,7 @@ __global__ __launch_bounds__(256) void k_spmm_bsr3(int nbr, const long long *__r
   const long long o = off[b >> 6];
   const int lane = b & 63;
   const int *bc = bcol + o + lane;
-  const double *bv = bval + 9 * o + lane;
+  const double *bv = bval + 9 * o + lane;  // + lane: the pair strips' offset 2 lane is added below
   double s[3][KC];
 #pragma unroll
   for (int r = 0; r < 3; ++r)
@@ -333,8 +333,15 @@ __global__ __launch_bounds__(256) void k_spmm_bsr3(int nbr, const long long *__r
     for (int u = 0; u < J; ++u) {
       const int q = q0 + u < L ? q0 + u : L - 1;
       j[u] = bc[64LL * q];
+      // values 0..7 as four 16-byte loads of pair-interleaved strips, value 8 from its own strip
+      const double *vq = bv + 9 * 64LL * q;
 #pragma unroll
-      for (int e = 0; e < 9; ++e) v[u][e] = bv[64LL * (9 * q + e)];
+      for (int m = 0; m < 4; ++m) {
+        const d2 t = *(const d2 *)(vq + 128 * m + lane);
+        v[u][2 * m] = t.x;
+        v[u][2 * m + 1] = t.y;
+      }
+      v[u][8] = vq[512];
     }
 #pragma unroll
     for (int u = 0; u < J; ++u) {

@@ -560,7 +560,7 @@ bool make_bsr3(int n_local, const long long *rowptr, const int *lcols, const dou
       out.bcol[(size_t)(slot + lane)] = lcols[rowptr[3 * b] + 3 * s];
       for (int r = 0; r < 3; ++r)
         for (int e = 0; e < 3; ++e)
-          out.vals[(size_t)(9 * slot + 64 * (3 * r + e) + lane)] = lvals[rowptr[3 * b + r] + 3 * s + e];
+          out.vals[bsr3_val_index(slot, 3 * r + e, lane)] = lvals[rowptr[3 * b + r] + 3 * s + e];
     }
   }
   return true;

@@ -76,8 +76,8 @@ void make_sell64(int n_local, const long long *rowptr, const int *lcols, const d
 // three rows have identical sorted column lists consisting of complete triples 3j, 3j + 1,
 // 3j + 2 of owned columns.  Qualifying block rows are stored SELL-64 by block: slot s of the
 // 64 block rows of a chunk at off[chunk] + 64 s + lane holds the block's first column 3j in
-// bcol and its 9 values (row-major: row r, column e at 9 (off[chunk] + 64 s) + 64 (3 r + e)
-// + lane) in vals; len[b] = the block row's blocks (0 for a block row that does not qualify).
+// bcol and its 9 values (row-major, value 3 r + e at bsr3_val_index(off[chunk] + 64 s, 3 r + e,
+// lane)) in vals; len[b] = the block row's blocks (0 for a block row that does not qualify).
 // rest lists the rows of non-qualifying block rows (and a last partial triple) for the
 // row kernel.  Returns false when fewer than 7/8 of the rows qualify (format not used).
 struct Bsr3 {
@@ -89,6 +89,13 @@ struct Bsr3 {
   std::vector<int> rest;
 };
 bool make_bsr3(int n_local, const long long *rowptr, const int *lcols, const double *lvals, Bsr3 &out);
+// Where value e (= 3 r + c, row r and column c of the block) of the block at slot base S
+// (= off[chunk] + 64 s) for lane `lane` is stored: the first eight values of the 64 lanes as
+// four pair-interleaved strips (value 2 m and 2 m + 1 of a lane adjacent: one 16-byte load
+// each), the ninth as a plain strip -- 5 loads per block instead of 9.
+__host__ __device__ inline size_t bsr3_val_index(long long S, int e, int lane) {
+  return (size_t)(9 * S + (e < 8 ? 128 * (e >> 1) + 2 * lane + (e & 1) : 512 + lane));
+}
 
 // Row-pair templates for k_spmm_tpl (kernels.hip): a compressed form of the pair plan for
 // matrices whose row pairs repeat a small number of shapes (stencils: the interior pairs of
