@@ -142,8 +142,11 @@ struct March27Coef {
 // the (z +- 1) centres from the lane's own loads; pd planes of loads in flight (1..3), nl lines
 // per thread (1, 2: tiles of 4 nl lines).
 // uni (optional): the stencil is uniform in the sense of march27_check over the five groups --
-// one coefficient table for every pair, absent entries reading out-of-grid zeros -- so the
-// kernel keeps no per-lane coefficients or masks.
+// one coefficient table for every pair, absent entries reading out-of-grid zeros -- and its
+// full template uses exactly kMarch7Used, so the kernel keeps no per-lane coefficients or masks.
+constexpr unsigned long long kMarch7Used =
+    (1ULL << 1) | (1ULL << 4) | (1ULL << 7) | (1ULL << 10) | (0x3FULL << 12) | (1ULL << 19) | (1ULL << 22) |
+    (1ULL << 25) | (1ULL << 28);
 bool launch_spmm_march7(hipStream_t s, int n_local, const unsigned char *tid, const unsigned long long *grp, int ntpl,
                         const MarchGeom &geom, const double *vals, int nvals, MvDesc X, MvDesc Y, double alpha,
                         double beta, const double *colscale = nullptr, int sz = 0, int pd = 2, int nl = 1,

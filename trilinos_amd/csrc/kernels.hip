@@ -1464,12 +1464,13 @@ __global__ __launch_bounds__(256) void k_spmm_march7(int npairs, int n_local, co
             const d2 ctr[5] = {om[l], ym, oz[l], yp, op[l]};
             double sa = 0.0, sb = 0.0;
             if constexpr (UNI) {
-              // uniform stencil: every pair adds the full template's products (absent entries
-              // read out-of-grid zeros); slots the full template does not use are skipped
-              auto uw = [&](int g, int i) __attribute__((always_inline)) {
-                return U.two_valued ? ((U.sel >> (6 * g + i)) & 1ULL ? U.v2[1] : U.v2[0]) : U.w[g][i];
-              };
-              auto on = [&](int g, int i) __attribute__((always_inline)) { return ((U.used >> (6 * g + i)) & 1ULL) != 0; };
+              // uniform stencil with the full 7-point pattern (kMarch7Used: the x line's six
+              // slots, c.lo / c.hi for the y / z groups): every pair adds the full template's
+              // products (absent entries read out-of-grid zeros) with the coefficients as kernel
+              // constants -- no per-slot tests (measured: the runtime tests were ~95 scalar
+              // instructions per 64 pairs and column, more than the VALU work)
+              auto uw = [&](int g, int i) __attribute__((always_inline)) { return U.w[g][i]; };
+              auto on = [&](int g, int i) __attribute__((always_inline)) { return ((kMarch7Used >> (6 * g + i)) & 1ULL) != 0; };
 #pragma unroll
               for (int g = 0; g < 5; ++g) {
                 const d2 x = ctr[g];

@@ -874,7 +874,7 @@ static void setup_template_kernels(migmres_crs *A, const PairTemplates &pt) {
     }
   }
   bool uni27 = uniform && Gu == 9;
-  bool uni7 = uniform && Gu == 5 && !env_on("MIGMRES_MARCH7_LANE_COEF");
+  bool uni7 = uniform && Gu == 5 && U.used == kMarch7Used && !env_on("MIGMRES_MARCH7_LANE_COEF");
   if (uniform && !env_on("MIGMRES_MARCH27_TABLE")) {  // at most two distinct values: select, not a table
     int nv = 0;
     for (int g = 0; g < Gu; ++g)
