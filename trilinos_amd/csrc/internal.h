@@ -128,10 +128,14 @@ bool launch_spmm_march(hipStream_t s, int n_local, const unsigned char *tid, con
 // The march for a UNIFORM 27-point stencil (G = 9 groups over every (plane, line) offset in
 // {-1, 0, 1}^2): one coefficient table U (slot i of group g) for every templated pair, the
 // slots a template leaves unused reading only neighbours outside the grid (march27_check).
+// The two diagonal slots of the 27-point pattern: the centre group (g = 4), row 0's c.lo and
+// row 1's c.hi.
+constexpr unsigned long long kMarch27Diag = (1ULL << 25) | (1ULL << 28);
 struct March27Coef {
   double w[9][6];
-  // two_valued: every w[g][i] is v2[(sel >> (6 g + i)) & 1] (Galeri's stencils: centre and
-  // neighbour value), so the kernel keeps 2 values instead of 54 in scalar registers
+  // two_valued (27-point only): every w[g][i] is v2[(sel >> (6 g + i)) & 1] with sel =
+  // kMarch27Diag (Brick3D: diagonal and neighbour value), so the kernel keeps 2 values
+  // instead of 54 in scalar registers
   int two_valued = 0;
   double v2[2] = {0.0, 0.0};
   unsigned long long sel = 0;

@@ -1708,8 +1708,10 @@ __global__ __launch_bounds__(256) void k_spmm_march27(int npairs, int n_local, c
               const d2 *b = pl + (bq - 1) * kMarchLX;
               const d2 x = b[0];
               const double left = b[-1].y, right = b[1].x;
+              // TWO: the Brick3D pattern (kMarch27Diag: v2[1] on the two diagonal slots, v2[0]
+              // elsewhere) fixed at compile time -- no per-slot scalar selects
               auto w = [&](int i) __attribute__((always_inline)) {
-                return TWO ? ((U.sel >> (6 * g + i)) & 1ULL ? U.v2[1] : U.v2[0]) : U.w[g][i];
+                return TWO ? ((kMarch27Diag >> (6 * g + i)) & 1ULL ? U.v2[1] : U.v2[0]) : U.w[g][i];
               };
               sa = sa + w(0) * left;
               sa = sa + w(1) * x.x;

@@ -888,7 +888,14 @@ static void setup_template_kernels(migmres_crs *A, const PairTemplates &pt) {
         if (which < 0) nv = 3;
         if (which == 1) U.sel |= 1ULL << (6 * g + i);
       }
-    U.two_valued = nv <= 2 ? 1 : 0;
+    // the 27-point kernel's two-valued form has the slot pattern fixed: the diagonal slots
+    // take v2[1], every other slot v2[0]
+    if (nv == 2 && U.sel == (((1ULL << 54) - 1) & ~kMarch27Diag)) {
+      std::swap(U.v2[0], U.v2[1]);
+      U.sel = kMarch27Diag;
+    }
+    U.two_valued = (nv <= 2 && (nv == 1 || U.sel == kMarch27Diag) && Gu == 9) ? 1 : 0;
+    if (nv == 1) U.v2[1] = U.v2[0];
     if (!U.two_valued) U.sel = 0;
   }
   const bool use_march = !env_on("MIGMRES_NO_MARCH") && groups && (generic || seven || uni27) && mg.nxp > 0 &&
