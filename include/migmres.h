@@ -299,7 +299,8 @@ int migmres_prec_diagonal(const migmres_prec *M, double *dinv_out);
  * over Ifpack2_Details_Chebyshev_def.hpp): the parameter list of Details::Chebyshev
  * (:280-300 defaults, setParameters :333-677) as plain fields.  max_eigenvalue NaN = not
  * given (estimate it: the power method on D^-1 A, :1341-1473, from an Epetra MINSTD random
- * vector with `seed` -- Tpetra's randomize() stream is not reproduced).  compute() (:739-896)
+ * vector with `seed` -- Tpetra's randomize() stream is not reproduced; a negative estimate is
+ * retried once from |x| of the stream's next draw, :1457-1471).  compute() (:739-896)
  * runs inside create; apply is migmres_prec_apply (ifpackApplyImpl :1221-1339, or
  * textbookApplyImpl :1163-1208 with textbook != 0). */
 typedef struct migmres_chebyshev_params {

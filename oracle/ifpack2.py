@@ -222,10 +222,10 @@ class Chebyshev:
         n = self.dinv.shape[0]
         if not self.p["chebyshev: assume matrix does not change"] or \
                 (np.isnan(self.computed_lmax) and np.isnan(self.user_lmax)):
-            x, _ = epetra_random_mv(self.seed, n, 1)
+            x, s2 = epetra_random_mv(self.seed, n, 1)
             lam = self.power_method(x[:, 0].copy())
-            if lam < 0.0:   # powerMethod (:1457-1471): retry once from |x|
-                x, _ = epetra_random_mv(self.seed, n, 1)
+            if lam < 0.0:   # powerMethod (:1457-1471): retry once from |x|, a new draw
+                x, _ = epetra_random_mv(s2, n, 1)
                 lam = self.power_method(np.abs(x[:, 0]))
             self.computed_lmax = lam
         lmax = self.computed_lmax if np.isnan(self.user_lmax) else float(self.user_lmax)

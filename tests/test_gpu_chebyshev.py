@@ -251,3 +251,54 @@ def test_block_gmres_with_chebyshev(comm, side):
     assert c["applies"] == ref["n_apply"] and c["prec_applies"] == ref["n_prec"]
     hist_close(sm.residualHistory(), ref["history"],
                oracle_rerun(ob.solve, Aor.apply, Bh, params, **{side: Mo}))
+
+
+def _block_rows(n, m, diag, off):
+    """Dense m x m diagonal blocks: diag on the diagonal, off elsewhere."""
+    def gen(first, nloc):
+        rp, gc, vv = [0], [], []
+        for i in range(first, first + nloc):
+            b = (i // m) * m
+            for j in range(b, min(n, b + m)):
+                gc.append(j)
+                vv.append(diag if j == i else off)
+            rp.append(len(gc))
+        return np.array(rp, dtype=np.int64), np.array(gc, dtype=np.int64), np.array(vv)
+    return gen
+
+
+def test_chebyshev_nan_estimate_fails_compute(comm):
+    """compute() throws when the max-eigenvalue estimate is Inf or NaN
+    (Ifpack2_Details_Chebyshev_def.hpp:828-833); ADVICE r3."""
+    import trilinos_amd as ta
+    n = 64
+    base = _block_rows(n, 4, 2.0, -0.5)
+
+    def gen(first, nloc):
+        rp, gc, vv = base(first, nloc)
+        vv = vv.copy()
+        vv[0] = np.nan
+        return rp, gc, vv
+    A = ta.CrsMatrix(comm, n, *gen(0, n))
+    M = ta.Chebyshev(A)
+    M.setParameters({"chebyshev: degree": 2})
+    M.initialize()
+    with pytest.raises(ta.MigmresError, match="Inf or NaN"):
+        M.compute()
+
+
+def test_chebyshev_negative_estimate_retries_with_next_draw(comm):
+    """D^-1 A = 2I - J on blocks of 8 has its dominant eigenvalue at -6, so the power method's
+    first estimate is negative and powerMethod retries from |x| of a NEW random vector
+    (:1457-1471: "try again with a different random initial guess") -- the next draw of the
+    same stream on both sides; 3 iterations keep the estimate sensitive to the start vector."""
+    from oracle import epetra as oe
+    n = 96
+    gen = _block_rows(n, 8, 0.5, -0.5)
+    params = {"chebyshev: degree": 2, "chebyshev: eigenvalue max iterations": 3}
+    B, _ = oe.epetra_random_mv(5, n, 1)
+    _, M = _oracle(gen, n, params, seed=3)
+    M(B)
+    assert M.computed_lmax < 0.0
+    _, _, _, computed = _device_apply(comm, gen, n, B, params, seed=3)
+    assert abs(computed - M.computed_lmax) <= 1e-13 * abs(M.computed_lmax)

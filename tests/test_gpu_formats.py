@@ -88,3 +88,18 @@ def test_device_formats_equal_host_formats(kind, dims, P, monkeypatch):
                   "noisy3D": "pair", "banded": "sell"}.get(kind)
         if expect:
             assert host[0][0] == expect
+
+
+@pytest.mark.parametrize("kind,dims", [("Laplace3D", (12, 11, 10)), ("Brick3D", (10, 9, 8))])
+def test_template_hash_collision_falls_back_to_host_builder(kind, dims, monkeypatch):
+    """A shape-hash collision in the device template builder (forced: MIGMRES_TPL_HASH_BITS=1
+    folds the 27 shapes onto two hashes) must not fail the CrsMatrix creation: the plan is
+    rebuilt by the host builder (exact shape comparison), so kernel and digest equal the host
+    path's (formats.hip threw on a collision and leaked the id buffer)."""
+    n, gen = _gen(kind, dims)
+    host = _stage(1, n, gen, False, monkeypatch, True)
+    monkeypatch.setenv("MIGMRES_TPL_HASH_BITS", "1")
+    dev = _stage(1, n, gen, False, monkeypatch, False)
+    devfc = _stage(1, n, gen, True, monkeypatch, False)
+    assert host[0][0] == dev[0][0] == devfc[0][0] == "march"
+    assert host[0][1] == dev[0][1] == devfc[0][1]

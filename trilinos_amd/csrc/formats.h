@@ -58,7 +58,9 @@ struct DevTemplates {
   std::vector<int> rec;
   std::vector<double> vals;
 };
-bool dev_templates(hipStream_t s, const DevCsr &A, DevTemplates &out);
+// 1: built; 0: not applicable (the host builder also declines); -1: two pair shapes share a
+// hash (nothing allocated): build this plan with make_pair_templates on the host instead.
+int dev_templates(hipStream_t s, const DevCsr &A, DevTemplates &out);
 
 // Pairs (by_pairs) or rows whose template id is kTplNone, ascending, into a new device array;
 // *rest_bytes = sum of 12 * length + 4 over their rows.

@@ -393,7 +393,7 @@ __device__ int tpl_shape(const int *rowptr, const int *cols, const double *vals,
 
 __global__ void k_tpl_hash(const int *rowptr, const int *cols, const double *vals, int n, int P,
                            const unsigned char *ghost, const unsigned long long *vkeys, const int *vslot, int nv,
-                           unsigned long long *hash, int *nk_out, int *pid) {
+                           unsigned long long hmask, unsigned long long *hash, int *nk_out, int *pid) {
   const int p = blockIdx.x * 256 + threadIdx.x;
   if (p >= P) return;
   pid[p] = p;
@@ -407,7 +407,7 @@ __global__ void k_tpl_hash(const int *rowptr, const int *cols, const double *val
     h = mix64d(h ^ (unsigned long long)(unsigned)off) + 0x632BE59BD9B4E019ULL;
     h = mix64d(h ^ (unsigned long long)sl);
   });
-  h = mix64d(h ^ (unsigned long long)nk);
+  h = mix64d(h ^ (unsigned long long)nk) & hmask;  // hmask: all ones (a test may truncate it)
   hash[p] = h == ~0ULL ? ~0ULL - 1 : h;
   nk_out[p] = nk;
 }
@@ -598,22 +598,29 @@ bool dev_bsr3(hipStream_t s, const DevCsr &A, DevBsr3 &out) {
   return true;
 }
 
-bool dev_templates(hipStream_t s, const DevCsr &A, DevTemplates &out) {
+int dev_templates(hipStream_t s, const DevCsr &A, DevTemplates &out) {
   const int n = A.n_local, P = (n + 1) / 2;
   out = DevTemplates();
   out.npairs = P;
-  if (P <= 0) return false;
+  if (P <= 0) return 0;
+  // MIGMRES_TPL_HASH_BITS (tests only): keep that many low bits of the shape hash, so that
+  // distinct shapes collide and the collision exit below is exercised
+  unsigned long long hmask = ~0ULL;
+  if (const char *hb = std::getenv("MIGMRES_TPL_HASH_BITS")) {
+    const int b = std::atoi(hb);
+    if (b > 0 && b < 64) hmask = (1ULL << b) - 1;
+  }
   Buf bad((size_t)P), ghost((size_t)P), cnt(sizeof(long long) * P), eoff(sizeof(long long) * (P + 1));
   setup_mark("formats: templates");
   k_tpl_check<<<nblk(P), 256, 0, s>>>(A.rowptr, A.cols, n, P, bad.as<unsigned char>(), ghost.as<unsigned char>(),
                                        cnt.as<long long>());
   MIG_HIP(hipGetLastError());
-  if (dev_max<unsigned char>(s, bad.as<unsigned char>(), P, 0)) return false;
+  if (dev_max<unsigned char>(s, bad.as<unsigned char>(), P, 0)) return 0;
   dev_offsets(s, cnt.as<long long>(), eoff.as<long long>(), P);
   long long m = 0;
   MIG_HIP(hipMemcpyAsync(&m, eoff.as<long long>() + P, sizeof(long long), hipMemcpyDeviceToHost, s));
   MIG_HIP(hipStreamSynchronize(s));
-  if (m == 0) return false;  // no pair without a ghost column
+  if (m == 0) return 0;  // no pair without a ghost column
   MIG_CHECK(m < (1LL << 31), "template plan: too many entries");
   // value dictionary: the distinct bit patterns in order of first appearance over the host
   // builder's visiting order (a stable sort by value keeps each value's visits in order)
@@ -632,7 +639,7 @@ bool dev_templates(hipStream_t s, const DevCsr &A, DevTemplates &out) {
     const int nd = dev_select(s, sbits.as<unsigned long long>(), head.as<unsigned char>(), mi,
                               ubits.as<unsigned long long>());
     dev_select(s, svid.as<long long>(), head.as<unsigned char>(), mi, uvid.as<long long>());
-    if (nd > 255) return false;
+    if (nd > 255) return 0;
     vkeys_h.resize((size_t)nd);
     std::vector<long long> first((size_t)nd);
     MIG_HIP(hipMemcpyAsync(vkeys_h.data(), ubits.p, sizeof(unsigned long long) * nd, hipMemcpyDeviceToHost, s));
@@ -656,11 +663,11 @@ bool dev_templates(hipStream_t s, const DevCsr &A, DevTemplates &out) {
   Buf hash(sizeof(unsigned long long) * P), nk(sizeof(int) * P), pid(sizeof(int) * P),
       shash(sizeof(unsigned long long) * P), spid(sizeof(int) * P), head((size_t)P);
   k_tpl_hash<<<nblk(P), 256, 0, s>>>(A.rowptr, A.cols, A.vals, n, P, ghost.as<unsigned char>(),
-                                      vkeys.as<unsigned long long>(), vslot.as<int>(), nv,
+                                      vkeys.as<unsigned long long>(), vslot.as<int>(), nv, hmask,
                                       hash.as<unsigned long long>(), nk.as<int>(), pid.as<int>());
   MIG_HIP(hipGetLastError());
   const int maxnk = dev_max<int>(s, nk.as<int>(), P, 0);
-  if (maxnk > kTplMaxKeys) return false;
+  if (maxnk > kTplMaxKeys) return 0;
   dev_sort_pairs(s, hash.as<unsigned long long>(), shash.as<unsigned long long>(), pid.as<int>(), spid.as<int>(), P);
   k_run_heads_u64<<<nblk(P), 256, 0, s>>>(shash.as<unsigned long long>(), P, head.as<unsigned char>());
   Buf uh(sizeof(unsigned long long) * P), up(sizeof(int) * P);
@@ -676,8 +683,8 @@ bool dev_templates(hipStream_t s, const DevCsr &A, DevTemplates &out) {
     tp.pop_back();
     --nh;
   }
-  if (nh == 0) return false;
-  if (nh > kTplMaxTemplates) return false;
+  if (nh == 0) return 0;
+  if (nh > kTplMaxTemplates) return 0;
   std::vector<int> order((size_t)nh), tslot((size_t)nh), trep((size_t)nh);
   for (int i = 0; i < nh; ++i) order[(size_t)i] = i;
   std::sort(order.begin(), order.end(), [&](int a, int b) { return tp[(size_t)a] < tp[(size_t)b]; });
@@ -695,8 +702,13 @@ bool dev_templates(hipStream_t s, const DevCsr &A, DevTemplates &out) {
                                         hash.as<unsigned long long>(), tkeys.as<unsigned long long>(), tsl.as<int>(),
                                         trp.as<int>(), nh, out.id, mism.as<unsigned char>());
   MIG_HIP(hipGetLastError());
-  MIG_CHECK(dev_max<unsigned char>(s, mism.as<unsigned char>(), P, 0) == 0,
-            "device template plan: a shape hash collision (set MIGMRES_HOST_FORMATS=1)");
+  if (dev_max<unsigned char>(s, mism.as<unsigned char>(), P, 0) != 0) {
+    // two shapes share a hash: no device plan; the caller builds this one on the host
+    MIG_HIP(hipStreamSynchronize(s));
+    MIG_HIP(hipFree(out.id));
+    out.id = nullptr;
+    return -1;
+  }
   out.ntpl = nh;
   out.maxk = std::max(maxnk, 1);
   {
@@ -709,7 +721,7 @@ bool dev_templates(hipStream_t s, const DevCsr &A, DevTemplates &out) {
   out.rec.resize(2 * (size_t)nh * out.maxk);
   MIG_HIP(hipMemcpyAsync(out.rec.data(), rec.p, sizeof(int) * out.rec.size(), hipMemcpyDeviceToHost, s));
   MIG_HIP(hipStreamSynchronize(s));
-  return true;
+  return 1;
 }
 
 int dev_template_rest(hipStream_t s, const DevCsr &A, const unsigned char *id, int npairs, bool by_pairs, int **out,

@@ -91,6 +91,11 @@ static void chebyshev_apply(migmres_prec &M, const migmres_mv &B, migmres_mv &X)
     launch_jacobi(c->stream, B.desc(), X.desc(), M.d_dinv, 1.0, n, false);
     return;
   }
+  // Chebyshev::apply (Ifpack2_Details_Chebyshev_def.hpp:920-932)
+  MIG_CHECK(std::isfinite(M.cheb_lmax), "Ifpack2::Chebyshev::apply: There is no estimate for the max eigenvalue.");
+  MIG_CHECK(std::isfinite(M.cheb_lmin), "Ifpack2::Chebyshev::apply: There is no estimate for the min eigenvalue.");
+  MIG_CHECK(std::isfinite(M.cheb_ratio),
+            "Ifpack2::Chebyshev::apply: There is no estimate for the ratio of the max eigenvalue to the min eigenvalue.");
   const double alpha = M.cheb_lmax / M.cheb_ratio;
   const double beta = p.boost_factor * M.cheb_lmax;
   const double delta = 2.0 / (beta - alpha);
@@ -151,12 +156,14 @@ static void chebyshev_compute(migmres_prec &M) {
     unsigned seed = p.seed;
     mv_random(*x, &seed);
     double lmax = power_method(M, *x, *y);
-    if (lmax < 0.0) {  // powerMethod (:1457-1471): once more from |random|
-      seed = p.seed;
+    if (lmax < 0.0) {  // powerMethod (:1457-1471): once more from |random|, the next draw of the stream
       mv_random(*x, &seed);
       launch_abs(M.ctx->stream, x->desc(), M.A->n_local);  // PositivizeVector (:191-221)
       lmax = power_method(M, *x, *y);
     }
+    MIG_CHECK(std::isfinite(lmax),
+              "Ifpack2::Chebyshev::compute: Estimation of the max eigenvalue of D^{-1} A failed, by producing Inf "
+              "or NaN.  This probably means that the matrix contains Inf or NaN values, or that it is badly scaled.");
     M.cheb_computed_lmax = lmax;
   }
   M.cheb_lmax = std::isnan(p.max_eigenvalue) ? M.cheb_computed_lmax : p.max_eigenvalue;

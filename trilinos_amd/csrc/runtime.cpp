@@ -942,6 +942,43 @@ static void setup_template_kernels(migmres_crs *A, const PairTemplates &pt) {
   }
 }
 
+// make_pair_templates (plan.cpp) on a host copy of the local CRS, uploaded with the pairs
+// left to the rest kernel.  Returns false (nothing changed) when the shapes do not fit.
+static bool install_templates_host(migmres_crs *A, const long long *rowptr, const int *lcols, const double *lvals) {
+  const int n_local = A->n_local;
+  PairTemplates pt;
+  if (!make_pair_templates(n_local, rowptr, lcols, lvals, pt)) return false;
+  std::vector<int> rest;
+  double rest_bytes = 0.0;
+  for (int q = 0; q < pt.npairs; ++q) {
+    if (pt.id[(size_t)q] != kTplNone) continue;
+    if (A->use_pairs) rest.push_back(q);
+    for (int r = 2 * q; r < std::min(n_local, 2 * q + 2); ++r) {
+      if (!A->use_pairs) rest.push_back(r);
+      rest_bytes += 12.0 * (double)(rowptr[r + 1] - rowptr[r]) + 4.0;
+    }
+  }
+  MIG_HIP(hipMalloc(&A->d_tpl_id, pt.id.size()));
+  MIG_HIP(hipMalloc(&A->d_tpl_rec, sizeof(int) * pt.rec.size()));
+  MIG_HIP(hipMalloc(&A->d_tpl_val, sizeof(double) * (pt.vals.size() + 1)));
+  MIG_HIP(hipMemcpy(A->d_tpl_id, pt.id.data(), pt.id.size(), hipMemcpyHostToDevice));
+  MIG_HIP(hipMemcpy(A->d_tpl_rec, pt.rec.data(), sizeof(int) * pt.rec.size(), hipMemcpyHostToDevice));
+  if (!pt.vals.empty())
+    MIG_HIP(hipMemcpy(A->d_tpl_val, pt.vals.data(), sizeof(double) * pt.vals.size(), hipMemcpyHostToDevice));
+  if (!rest.empty()) {
+    MIG_HIP(hipMalloc(&A->d_tpl_rest, sizeof(int) * rest.size()));
+    MIG_HIP(hipMemcpy(A->d_tpl_rest, rest.data(), sizeof(int) * rest.size(), hipMemcpyHostToDevice));
+  }
+  A->n_tpl_rest = (int)rest.size();
+  A->tpl_ntpl = pt.ntpl;
+  A->tpl_maxk = pt.maxk;
+  A->tpl_nvals = (int)pt.vals.size();
+  A->use_tpl = true;
+  setup_template_kernels(A, pt);
+  A->spmm_fixed_bytes = (double)pt.npairs + 8.0 * pt.rec.size() / 2 + 8.0 * pt.vals.size() + rest_bytes;
+  return true;
+}
+
 // formats.hip: every SpMM format plan and the halo overlap's unit lists from the device CSR.
 static void build_formats_device(migmres_crs *A) {
   migmres_ctx *ctx = A->ctx;
@@ -983,7 +1020,19 @@ static void build_formats_device(migmres_crs *A) {
   }
   A->spmm_fixed_bytes = A->use_bsr3 ? A->b3_fixed_bytes : 12.0 * nnz + 4.0 * (n_local + 1);
   DevTemplates dt;
-  if (!env_on("MIGMRES_NO_TPL_SPMM") && n_local > 0 && dev_templates(s, dc, dt)) {
+  const int tpl = !env_on("MIGMRES_NO_TPL_SPMM") && n_local > 0 ? dev_templates(s, dc, dt) : 0;
+  if (tpl < 0) {
+    // two shapes share a hash: the host builder (exact shape comparison) on a copy of the CRS
+    ++A->tpl_host_fallbacks;
+    std::vector<int> rp32((size_t)n_local + 1), lcols((size_t)nnz);
+    std::vector<double> lvals((size_t)nnz);
+    MIG_HIP(hipMemcpy(rp32.data(), A->d_rowptr, sizeof(int) * rp32.size(), hipMemcpyDeviceToHost));
+    MIG_HIP(hipMemcpy(lcols.data(), A->d_cols, sizeof(int) * lcols.size(), hipMemcpyDeviceToHost));
+    MIG_HIP(hipMemcpy(lvals.data(), A->d_vals, sizeof(double) * lvals.size(), hipMemcpyDeviceToHost));
+    std::vector<long long> rp(rp32.begin(), rp32.end());
+    install_templates_host(A, rp.data(), lcols.data(), lvals.data());
+  }
+  if (tpl > 0) {
     double rest_bytes = 0.0;
     A->n_tpl_rest = dev_template_rest(s, dc, dt.id, dt.npairs, A->use_pairs, &A->d_tpl_rest, &rest_bytes);
     A->d_tpl_id = dt.id;
@@ -1146,42 +1195,8 @@ static void crs_finish(migmres_crs *A, const long long *rowptr, std::vector<int>
         }
       }
       A->spmm_fixed_bytes = A->use_bsr3 ? A->b3_fixed_bytes : 12.0 * nnz + 4.0 * (n_local + 1);
-      {
-        // row-pair templates: the pairs' shapes repeat (stencils) -> one byte per pair
-        const char *nt = std::getenv("MIGMRES_NO_TPL_SPMM");
-        PairTemplates pt;
-        if (!(nt && nt[0] == '1') && n_local > 0 &&
-            make_pair_templates(n_local, rowptr, lcols.data(), lvals.data(), pt)) {
-          std::vector<int> rest;
-          double rest_bytes = 0.0;
-          for (int q = 0; q < pt.npairs; ++q) {
-            if (pt.id[(size_t)q] != kTplNone) continue;
-            if (A->use_pairs) rest.push_back(q);
-            for (int r = 2 * q; r < std::min(n_local, 2 * q + 2); ++r) {
-              if (!A->use_pairs) rest.push_back(r);
-              rest_bytes += 12.0 * (double)(rowptr[r + 1] - rowptr[r]) + 4.0;
-            }
-          }
-          MIG_HIP(hipMalloc(&A->d_tpl_id, pt.id.size()));
-          MIG_HIP(hipMalloc(&A->d_tpl_rec, sizeof(int) * pt.rec.size()));
-          MIG_HIP(hipMalloc(&A->d_tpl_val, sizeof(double) * (pt.vals.size() + 1)));
-          MIG_HIP(hipMemcpy(A->d_tpl_id, pt.id.data(), pt.id.size(), hipMemcpyHostToDevice));
-          MIG_HIP(hipMemcpy(A->d_tpl_rec, pt.rec.data(), sizeof(int) * pt.rec.size(), hipMemcpyHostToDevice));
-          if (!pt.vals.empty())
-            MIG_HIP(hipMemcpy(A->d_tpl_val, pt.vals.data(), sizeof(double) * pt.vals.size(), hipMemcpyHostToDevice));
-          if (!rest.empty()) {
-            MIG_HIP(hipMalloc(&A->d_tpl_rest, sizeof(int) * rest.size()));
-            MIG_HIP(hipMemcpy(A->d_tpl_rest, rest.data(), sizeof(int) * rest.size(), hipMemcpyHostToDevice));
-          }
-          A->n_tpl_rest = (int)rest.size();
-          A->tpl_ntpl = pt.ntpl;
-          A->tpl_maxk = pt.maxk;
-          A->tpl_nvals = (int)pt.vals.size();
-          A->use_tpl = true;
-          setup_template_kernels(A, pt);
-          A->spmm_fixed_bytes = (double)pt.npairs + 8.0 * pt.rec.size() / 2 + 8.0 * pt.vals.size() + rest_bytes;
-        }
-      }
+      // row-pair templates: the pairs' shapes repeat (stencils) -> one byte per pair
+      if (!env_on("MIGMRES_NO_TPL_SPMM") && n_local > 0) install_templates_host(A, rowptr, lcols.data(), lvals.data());
       if (n_remote > 0) {
         // interior / boundary units for the halo overlap (a unit is a row pair with the
         // row-pair kernel, else a row; boundary = reads at least one ghost column)

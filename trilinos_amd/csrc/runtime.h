@@ -165,6 +165,7 @@ struct migmres_crs {
   double *d_tpl_val = nullptr;
   int tpl_ntpl = 0, tpl_maxk = 0, tpl_nvals = 0;
   bool use_tpl = false;
+  int tpl_host_fallbacks = 0;  // device template plans rebuilt on the host after a shape-hash collision
   int *d_tpl_rest = nullptr;
   // stencil-group form of the templates (k_spmm_tpl3: one X load per key triple, the
   // neighbours' halves by DPP lane shifts) when the keys come in x-neighbour triples
