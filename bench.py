@@ -105,6 +105,49 @@ def pmc_ratio(kernel_class, world):
         return None
 
 
+def csr_spmm_forms(ta, comm, args, n, k, nnz, call, reps=20):
+    """The same operator built again with the stencil formats switched off (the environment
+    switches are read at creation), and `reps` applies of X (k columns) timed through the
+    library's HIP-event profile: the row-pair CSR kernel (MIGMRES_NO_TPL_SPMM) and the plain
+    thread-per-row CSR kernel (also MIGMRES_NO_PAIR_SPMM, MIGMRES_NO_SELL_SPMM).  Fractions on
+    the CSR's bytes 12 nnz + 4 (N + 1) + 16 N k."""
+    import ctypes as C
+    forms = {"csr_pair": {"MIGMRES_NO_TPL_SPMM": "1"},
+             "csr_row": {"MIGMRES_NO_TPL_SPMM": "1", "MIGMRES_NO_PAIR_SPMM": "1", "MIGMRES_NO_SELL_SPMM": "1"}}
+    csr_bytes = 12.0 * nnz + 4.0 * (n + 1) + 16.0 * n * k
+    res = {}
+    for name, env in forms.items():
+        old = {key: os.environ.get(key) for key in env}
+        os.environ.update(env)
+        try:
+            if args.matrix == "FlanProxy":
+                A2 = ta.CrsMatrix.galeri(comm, "FlanProxy", 81, 81, 80)
+            else:
+                A2 = ta.CrsMatrix.galeri(comm, args.matrix, args.nx, args.nx, args.nx)
+        finally:
+            for key, v in old.items():
+                if v is None:
+                    os.environ.pop(key, None)
+                else:
+                    os.environ[key] = v
+        X2, Y2 = ta.MultiVector(comm, n, k), ta.MultiVector(comm, n, k)
+        X2.random(5)
+        A2.apply(X2, Y2)  # warm
+        call("migmres_ctx_profile", comm.h, 1)
+        for _ in range(reps):
+            A2.apply(X2, Y2)
+        nk = 32
+        ms, by, cnt = (C.c_double * nk)(), (C.c_double * nk)(), (C.c_longlong * nk)()
+        call("migmres_ctx_profile_read", comm.h, ms, by, cnt, nk)
+        call("migmres_ctx_profile", comm.h, 0)
+        i = [j for j in range(nk) if cnt[j]]
+        t = sum(ms[j] for j in i) / 1e3 / reps
+        res[name] = {"kernel": A2.spmm_kernel(), "mean_launch_us": t * 1e6, "csr_bytes": csr_bytes,
+                     "achieved": csr_bytes / t / 1e9, "frac": csr_bytes / t / 1e9 / HBM_PEAK_GBPS}
+        del A2, X2, Y2
+    return res
+
+
 def spawn_ranks(n, argv, port=None, timeout=None, poll_s=0.1):
     """`bench.py --gpus N` without a torchrun environment: start N rank processes of this
     script (one per GPU, RANK = LOCAL_RANK = i, WORLD_SIZE = N, MASTER_ADDR 127.0.0.1) as
@@ -207,6 +250,8 @@ def main():
                          "(--cheb-degree, power-method lambda max)")
     ap.add_argument("--cheb-degree", type=int, default=3)
     ap.add_argument("--ortho", default="ICGS", choices=["ICGS", "DGKS"])
+    ap.add_argument("--no-csr-spmm", dest="csr_spmm", action="store_false",
+                    help="skip timing the CSR SpMM forms beside the default SpMM (roofline_spmm.csr_forms)")
     ap.add_argument("--comm-timeout", type=float, default=300.0,
                     help="seconds: torch.distributed (gloo) set-up / barrier timeout and the RCCL init watchdog")
     ap.add_argument("--deadline", type=float, default=1500.0,
@@ -340,8 +385,12 @@ def main():
            f"Jacobi({args.sweeps} sweeps) ") + f"{args.prec} preconditioner, fixed work (tol 0)"
           if args.prec != "none" else
           f"{mname} fp64, k={k} RHS, {args.solver} Num Blocks {nb}, {args.ortho}, fixed work (tol 0)")
+    # secondary workloads name their own operator / k in the metric (the headline keeps BASELINE's)
+    metric = METRIC if headline else (
+        f"{args.solver} iterations/sec + achieved HBM GB/s, {mname}"
+        + (f" + {args.prec} {args.prec_type}" if args.prec != "none" else "") + f", k={k} RHS")
     out = {
-        "metric": METRIC, "value": value, "unit": "iterations/s", "n_gpus": world, "steps": steps,
+        "metric": metric, "value": value, "unit": "iterations/s", "n_gpus": world, "steps": steps,
         "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / steps, "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "f64",
         "data": (f"{mname} from file, " if args.matrix_file else "synthetic (Galeri " + args.matrix + ", ")
@@ -384,6 +433,20 @@ def main():
         out["kernels"] = {kname: dict(ms=v["ms"], launches=v["launches"],
                                       GBps=v["bytes"] / (v["ms"] / 1e3) / 1e9 if v["ms"] > 0 else None)
                           for kname, v in kstats.items()}
+    if kstats and "spmm" in kstats and world == 1:
+        # SURVEY 8(d) / north star "fp64 CSR SpMV x 8": the default SpMM kernel on the bytes it
+        # moves (its format's fixed bytes + X + Y, tallied per launch by the library), with the
+        # PMC traffic ratio of the committed profile, and the CSR kernels of the same operator
+        # timed beside it on the CSR's own bytes (12 nnz + 4 (N + 1) + 16 N k)
+        st = kstats["spmm"]
+        b, t = st["bytes"] / st["launches"], st["ms"] / 1e3 / st["launches"]
+        ratio = pmc_ratio("spmm", world) if headline else None
+        out["roofline_spmm"] = {"kernel": A.spmm_kernel(), "bound": "hbm", "achieved": b / t / 1e9,
+                                "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": b / t / 1e9 / HBM_PEAK_GBPS,
+                                "bytes_per_launch": b, "mean_launch_us": t * 1e6,
+                                "traffic": None if ratio is None else ratio * b, "traffic_ratio_pmc": ratio}
+        if args.csr_spmm and not args.matrix_file:
+            out["roofline_spmm"]["csr_forms"] = csr_spmm_forms(ta, comm, args, n, k, nnz_total, call)
     if headline:
         # SURVEY.md 8(d)'s model of the REFERENCE algorithm's traffic (column-by-column
         # findBasis, unfused updates) over the same wall time: a reference-equivalent rate,

@@ -43,6 +43,7 @@ typedef struct migmres_crs migmres_crs;
 typedef struct migmres_mv migmres_mv;
 typedef struct migmres_solver migmres_solver;
 typedef struct migmres_prec migmres_prec;
+typedef struct migmres_op migmres_op;
 
 /* error codes */
 #define MIGMRES_OK 0
@@ -51,6 +52,7 @@ typedef struct migmres_prec migmres_prec;
 #define MIGMRES_ERCCL -3
 #define MIGMRES_ENOMEM -4
 #define MIGMRES_ESTATE -5
+#define MIGMRES_EOP -6 /* a user operator's callback returned nonzero */
 
 /* norm types (Belos::NormType, belos/src/BelosTypes.hpp) */
 #define MIGMRES_ONE_NORM 0
@@ -180,6 +182,19 @@ int migmres_crs_import_plan(const migmres_crs *A, int *export_lids, int *export_
                             int *remote_lids, int *remote_pids);
 /* OperatorTraits::Apply / Tpetra apply: Y = alpha*A*X + beta*Y (beta==0 ignores Y). */
 int migmres_crs_apply(migmres_crs *A, const migmres_mv *X, migmres_mv *Y, double alpha, double beta);
+/* Tpetra::CrsMatrix::apply(X, Y, mode, alpha, beta) (tpetra/core/src/Tpetra_CrsMatrix_def.hpp:
+ * 5176-5208) / Epetra_CrsMatrix::Multiply(TransA, X, Y) (epetra/src/Epetra_CrsMatrix.cpp:
+ * 3107-3285) with the transpose: Y = alpha*A^T*X + beta*Y.  A^T runs GeneralMTM's scatter order
+ * (:3587-3650: y = 0, then row by row y[col] += v*x[row]) as a row kernel over a transpose built
+ * on the device at the first call; on several ranks the contributions to ghost columns go back
+ * to their owners (Epetra_Export, combine Add), added in ascending PID order, then alpha and
+ * beta are applied (alpha 1, beta 0 = Epetra's Multiply(true, ...) bit for bit).  X and Y may
+ * not alias (Tpetra localApply's check).  OperatorTraits::HasApplyTranspose = true. */
+#define MIGMRES_NO_TRANS 0
+#define MIGMRES_TRANS 1
+#define MIGMRES_CONJ_TRANS 2
+int migmres_crs_apply_mode(migmres_crs *A, const migmres_mv *X, migmres_mv *Y, int mode, double alpha,
+                           double beta);
 /* Which SpMM kernel apply() runs for this operator (chosen at creation from the local rows):
  * MIGMRES_SPMM_CSR thread per row over the CSR, MIGMRES_SPMM_PAIR row pairs with 16-byte X
  * loads (rows of <= 8 entries), MIGMRES_SPMM_SELL thread per row over a SELL-64 copy,
@@ -208,6 +223,26 @@ int migmres_crs_spmm_kernel(const migmres_crs *A, int *kind);
  * format array -- into out[0 .. n); *needed = the digest count.  Test support: the device
  * builders (formats.hip) and the host builders (MIGMRES_HOST_FORMATS=1, plan.cpp) must agree. */
 int migmres_crs_format_digest(const migmres_crs *A, unsigned long long *out, int n, int *needed);
+
+/* ---------------- user operators (Belos::OperatorTraits<double, MV, OP> for any OP) ----------------
+ * An operator the library does not hold as a CRS: Y = op(X) through a host callback
+ * (BelosOperatorTraits.hpp:108-155; the reference solves with any Epetra_Operator /
+ * Tpetra::Operator, BelosLinearProblem.hpp:989-1072).  The callback receives the library's
+ * own multivector handles (views into the Krylov basis among them) and must leave Y complete in
+ * the stream order of the context's stream: a callback that only calls migmres_* functions on
+ * the same context does (they enqueue on that stream) -- including a whole nested
+ * migmres_solver_solve_op, as the reference's Iterative_Inverse_Operator does
+ * (belos/epetra/test/BlockGmres/test_bl_gmres_diag.cpp:233-305); work on another stream must be
+ * synchronised before it returns.  A nonzero return fails the apply (and the solve) with
+ * MIGMRES_EOP.  The solver does not re-apply a user operator to regenerate a block (it keeps a
+ * copy, as the reference does) and never applies one speculatively. */
+typedef int (*migmres_apply_fn)(void *user, const migmres_mv *X, migmres_mv *Y);
+int migmres_op_create(migmres_ctx *ctx, long long n_global, int n_local, migmres_apply_fn fn, void *user,
+                      migmres_op **out);
+/* The CRS operator as a migmres_op (borrowed: A must outlive it); solve_op on it = solve(A). */
+int migmres_op_from_crs(migmres_crs *A, migmres_op **out);
+int migmres_op_apply(migmres_op *op, const migmres_mv *X, migmres_mv *Y);
+int migmres_op_destroy(migmres_op *op);
 
 /* ---------------- multivectors (Belos::MultiVecTraits) ---------------- */
 
@@ -386,6 +421,11 @@ int migmres_solver_set_prec(migmres_solver *s, int side, migmres_prec *M);
  * *converged = 1 for Belos::Converged, 0 for Unconverged. */
 int migmres_solver_solve(migmres_solver *s, migmres_crs *A, migmres_mv *X, const migmres_mv *B,
                          int *converged);
+/* The same with any operator (LinearProblem::setOperator of an OP that is not a CRS). */
+int migmres_solver_solve_op(migmres_solver *s, migmres_op *A, migmres_mv *X, const migmres_mv *B,
+                            int *converged);
+/* setLeftPrec / setRightPrec with a user operator (borrowed; NULL removes it). */
+int migmres_solver_set_prec_op(migmres_solver *s, int side, migmres_op *M);
 int migmres_solver_num_iters(const migmres_solver *s, int *iters);
 int migmres_solver_achieved_tol(const migmres_solver *s, double *tol);
 int migmres_solver_loa_detected(const migmres_solver *s, int *loa);

@@ -162,10 +162,10 @@ struct MVT {
 // Belos::OperatorTraits<double, MV, Op> (belos/src/BelosOperatorTraits.hpp:108-155).
 struct OPT {
   static void Apply(const Op &op, const MV &x, MV &y, ETrans trans = NOTRANS) {
-    if (trans != NOTRANS) throw Failure(MIGMRES_EINVAL, "OperatorTraits::Apply: transpose not provided");
-    check(migmres_crs_apply(op.A, x.get(), y.get(), 1.0, 0.0), "Apply");  // halo import + SpMM
+    const int mode = trans == NOTRANS ? MIGMRES_NO_TRANS : trans == TRANS ? MIGMRES_TRANS : MIGMRES_CONJ_TRANS;
+    check(migmres_crs_apply_mode(op.A, x.get(), y.get(), mode, 1.0, 0.0), "Apply");  // halo + SpMM (or A^T)
   }
-  static bool HasApplyTranspose(const Op &) { return false; }
+  static bool HasApplyTranspose(const Op &) { return true; }
 };
 
 }  // namespace migmres_belos

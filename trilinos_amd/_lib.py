@@ -26,6 +26,7 @@ P = C.POINTER
 
 # setUserConvStatusTest callback: (user, iters, nrhs, scaled residual norms) -> passed
 STATUS_FN = C.CFUNCTYPE(i32, vp, i32, i32, P(f64))
+APPLY_FN = C.CFUNCTYPE(i32, vp, vp, vp)
 
 # name: (argtypes)
 _SIGS = {
@@ -57,6 +58,7 @@ _SIGS = {
     "migmres_crs_colmap": [vp, P(i64)],
     "migmres_crs_import_plan": [vp, P(i32), P(i32), P(i32), P(i32)],
     "migmres_crs_apply": [vp, vp, vp, f64, f64],
+    "migmres_crs_apply_mode": [vp, vp, vp, i32, f64, f64],
     "migmres_crs_spmm_kernel": [vp, P(i32)],
     "migmres_mv_create": [vp, i64, i32, i32, P(vp)],
     "migmres_mv_view": [vp, P(i32), i32, P(vp)],
@@ -106,6 +108,12 @@ _SIGS = {
     "migmres_solver_reset": [vp, i32],
     "migmres_solver_set_user_conv_test": [vp, STATUS_FN, vp, i32],
     "migmres_solver_solve": [vp, vp, vp, vp, P(i32)],
+    "migmres_solver_solve_op": [vp, vp, vp, vp, P(i32)],
+    "migmres_solver_set_prec_op": [vp, i32, vp],
+    "migmres_op_create": [vp, C.c_longlong, i32, APPLY_FN, vp, P(vp)],
+    "migmres_op_from_crs": [vp, P(vp)],
+    "migmres_op_apply": [vp, vp, vp],
+    "migmres_op_destroy": [vp],
     "migmres_solver_num_iters": [vp, P(i32)],
     "migmres_solver_achieved_tol": [vp, P(f64)],
     "migmres_solver_loa_detected": [vp, P(i32)],

@@ -123,13 +123,15 @@ class MultiVecTraits:
 class OperatorTraits:
     @staticmethod
     def Apply(Op, x, y, trans=False):
+        """BelosOperatorTraits.hpp:108-155 (trans: NOTRANS / TRANS as a bool or 0/1/2)."""
         if trans:
-            raise NotImplementedError("transpose apply is not on the hot path")
-        Op.apply(x, y)
+            Op.apply(x, y, 1.0, 0.0, int(trans))
+        else:
+            Op.apply(x, y)
 
     @staticmethod
     def HasApplyTranspose(Op):
-        return False
+        return hasattr(Op, "multiply")
 
 
 class ICGSOrthoManager:
@@ -338,11 +340,16 @@ class BlockGmresSolMgr:
         if self.params["Orthogonalization"] not in ("ICGS", "DGKS"):
             raise NotImplementedError('device Block GMRES implements "Orthogonalization" = "ICGS" and "DGKS"')
         self._ensure()
+        from .linalg import Operator
         for side, M in ((0, self.problem.LP), (1, self.problem.RP)):
-            call("migmres_solver_set_prec", self.h, side, M.h if M is not None else None)
+            if isinstance(M, Operator):   # a user operator as the preconditioner
+                call("migmres_solver_set_prec_op", self.h, side, M.h)
+            else:
+                call("migmres_solver_set_prec_op", self.h, side, None)
+                call("migmres_solver_set_prec", self.h, side, M.h if M is not None else None)
         conv = C.c_int()
-        call("migmres_solver_solve", self.h, self.problem.A.h, self.problem.X.h,
-             self.problem.B.h, C.byref(conv))
+        fn = "migmres_solver_solve_op" if isinstance(self.problem.A, Operator) else "migmres_solver_solve"
+        call(fn, self.h, self.problem.A.h, self.problem.X.h, self.problem.B.h, C.byref(conv))
         return Converged if conv.value else Unconverged
 
     def getNumIters(self):

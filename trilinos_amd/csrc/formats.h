@@ -72,4 +72,15 @@ int dev_template_rest(hipStream_t s, const DevCsr &A, const unsigned char *id, i
 void dev_halo_units(hipStream_t s, const DevCsr &A, bool by_pairs, int **interior, int *n_interior, int **boundary,
                     int *n_boundary);
 
+// The local transpose for Y = A^T X (Epetra_CrsMatrix::Multiply(TransA = true) -> GeneralMTM,
+// epetra/src/Epetra_CrsMatrix.cpp:3587-3650): row c (an X-space column of A: owned row c, or
+// ghost slot c - n_local) lists A's entries (r, v) of column c in ascending r -- the order in
+// which GeneralMTM's scatter loop (y = 0; for i: for j: y[col_j] += v_j * x_i) adds them, so a
+// row-kernel SpMM over it reproduces the loop bit for bit.  Arrays allocated here.
+struct DevTrans {
+  int *rowptr = nullptr, *cols = nullptr;
+  double *vals = nullptr;
+};
+void dev_transpose(hipStream_t s, const DevCsr &A, int n_out, DevTrans &out);
+
 }  // namespace migmres

@@ -497,6 +497,32 @@ __global__ void k_unit_ghost(const int *rowptr, const int *cols, int n, int nuni
   inr[u] = g ? 0 : 1;
 }
 
+// ------------------------------------------------------------------ transpose (GeneralMTM order)
+__global__ void k_tr_rowid(const int *rowptr, int n, int *rowid, int *eid) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= n) return;
+  for (int e = rowptr[r]; e < rowptr[r + 1]; ++e) {
+    rowid[e] = r;
+    eid[e] = e;
+  }
+}
+__global__ void k_tr_count(const int *cols, long long nnz, unsigned long long *cnt) {
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (e < nnz) atomicAdd(&cnt[cols[e]], 1ULL);  // integer counts: order-independent
+}
+__global__ void k_tr_fill(const int *sorted_e, const int *rowid, const double *vals, long long nnz, int *tcols,
+                          double *tvals) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= nnz) return;
+  const int e = sorted_e[i];
+  tcols[i] = rowid[e];
+  tvals[i] = vals[e];
+}
+__global__ void k_tr_rowptr32(const long long *off, int n1, int *rp) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n1) rp[i] = (int)off[i];
+}
+
 }  // namespace
 
 void setup_mark(const char *what) {
@@ -756,6 +782,32 @@ void dev_halo_units(hipStream_t s, const DevCsr &A, bool by_pairs, int **interio
   MIG_HIP(hipGetLastError());
   *n_interior = dev_select_ids(s, inr.as<unsigned char>(), nunits, *interior);
   *n_boundary = dev_select_ids(s, bnd.as<unsigned char>(), nunits, *boundary);
+}
+
+void dev_transpose(hipStream_t s, const DevCsr &A, int n_out, DevTrans &out) {
+  const int n = A.n_local;
+  const long long nnz = A.nnz;
+  out = DevTrans();
+  MIG_HIP(hipMalloc(&out.rowptr, sizeof(int) * ((size_t)n_out + 1)));
+  MIG_HIP(hipMalloc(&out.cols, sizeof(int) * (size_t)(nnz > 0 ? nnz : 1)));
+  MIG_HIP(hipMalloc(&out.vals, sizeof(double) * (size_t)(nnz > 0 ? nnz : 1)));
+  Buf cnt(sizeof(long long) * ((size_t)n_out + 1)), off(sizeof(long long) * ((size_t)n_out + 2));
+  MIG_HIP(hipMemsetAsync(cnt.p, 0, sizeof(long long) * ((size_t)n_out + 1), s));
+  if (nnz > 0) {
+    Buf rowid(sizeof(int) * nnz), eid(sizeof(int) * nnz), skey(sizeof(int) * nnz), se(sizeof(int) * nnz);
+    k_tr_rowid<<<nblk(n), 256, 0, s>>>(A.rowptr, n, rowid.as<int>(), eid.as<int>());
+    k_tr_count<<<nblk(nnz), 256, 0, s>>>(A.cols, nnz, cnt.as<unsigned long long>());
+    MIG_HIP(hipGetLastError());
+    // stable by column: entries of one column keep their (row-major, hence ascending-row) order
+    dev_sort_pairs(s, A.cols, skey.as<int>(), eid.as<int>(), se.as<int>(), (int)nnz);
+    k_tr_fill<<<nblk(nnz), 256, 0, s>>>(se.as<int>(), rowid.as<int>(), A.vals, nnz, out.cols, out.vals);
+    MIG_HIP(hipGetLastError());
+    MIG_HIP(hipStreamSynchronize(s));
+  }
+  dev_offsets(s, cnt.as<long long>(), off.as<long long>(), n_out);
+  k_tr_rowptr32<<<nblk(n_out + 1), 256, 0, s>>>(off.as<long long>(), n_out + 1, out.rowptr);
+  MIG_HIP(hipGetLastError());
+  MIG_HIP(hipStreamSynchronize(s));
 }
 
 }  // namespace migmres

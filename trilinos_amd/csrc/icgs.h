@@ -25,8 +25,22 @@ struct IcgsState {
 // by launch_fbg_chol), block-major (partial[b * nv + i]) for k > 8 (launch_reduce_partials,
 // then launch_fbg_chol_l).  launch_gemm_nn_gram: k <= 8 only.
 // w: 768 doubles of device scratch (T1, T2, R1).
+// NngPro (optional): the small steps between blkOrtho's passes folded into the closing update's
+// prologue -- M = C1 + C2 formed as the coefficients are staged (k_add_coef's sum, same
+// rounding), workgroup 0 storing it to `cout` for the host, resetting the state and recording
+// oldDot = diag of the Gram block G (k_state_reset + k_blk_old): three launches fewer per block.
+struct NngPro {
+  const double *C1 = nullptr, *C2 = nullptr;  // null: M as given
+  int ld1 = 0, ld2 = 0;
+  double *cout = nullptr;
+  int ldo = 0;
+  IcgsState *st = nullptr;  // null: no state step
+  const double *G = nullptr;
+  int ldg = 0, dgks = 0;
+  double blk_tol = 0.0, sing_tol = 0.0, dep_tol = 0.0;
+};
 int launch_gemm_nn_gram(hipStream_t s, MvDesc A, int L, const double *M, int ldm, MvDesc X, int nrows,
-                        double *partial);
+                        double *partial, const NngPro &pro = NngPro());
 int launch_fbg_gram(hipStream_t s, MvDesc X, int k, int nrows, double *partial, int rev);
 int launch_fbg_a(hipStream_t s, MvDesc X, int k, int nrows, const IcgsState *st, const double *w, double *partial,
                  int rev);

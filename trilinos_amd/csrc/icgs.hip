@@ -1928,11 +1928,32 @@ __device__ __forceinline__ void fbg_apply(d2 (&x)[K], const double (&T)[16 * K])
 // row reads as zero, adds nothing to a Gram matrix and is not stored.
 template <int K>
 __global__ __launch_bounds__(FBG_NT) void k_gemm_nn_gram(MvDesc A, int L, const double *__restrict__ M, int ldm,
-                                                        MvDesc X, int nrows, double *__restrict__ partial) {
+                                                        MvDesc X, int nrows, double *__restrict__ partial,
+                                                        NngPro pro) {
   extern __shared__ __attribute__((aligned(16))) double Mg[];  // L x K
+  const bool first = blockIdx.x == 0;
   for (int e = threadIdx.x; e < L * K; e += FBG_NT) {
     const int j = e / K, c = e % K;
-    Mg[e] = M[j + (long long)c * ldm];
+    double m;
+    if (pro.C1) {
+      m = pro.C1[j + (long long)c * pro.ld1] + pro.C2[j + (long long)c * pro.ld2];  // k_add_coef's sum
+      if (first) pro.cout[j + (long long)c * pro.ldo] = m;
+    } else {
+      m = M[j + (long long)c * ldm];
+    }
+    Mg[e] = m;
+  }
+  if (first && pro.st && threadIdx.x == 0) {  // k_state_reset, then k_blk_old
+    IcgsState *st = pro.st;
+    st->dgks = pro.dgks;
+    st->dep_tol = pro.dep_tol;
+    st->failed = -1;
+    st->dep = 0.0;
+    st->neg = 0.0;
+    st->blk_tol = pro.blk_tol;
+    st->sing_tol = pro.sing_tol;
+    for (int i = 0; i < 256; ++i) st->B[i] = 0.0;
+    for (int c = 0; c < K; ++c) st->blk_old[c] = pro.G[(L + c) + (long long)c * pro.ldg];
   }
   __syncthreads();
   constexpr int NV = K * (K + 1) / 2, NB = 8;
@@ -2236,9 +2257,22 @@ __global__ __launch_bounds__(256) void k_fbg_chol(const double *__restrict__ par
   double v[NV];
 #pragma unroll
   for (int i = 0; i < NV; ++i) v[i] = 0.0;
-  for (int b = threadIdx.x; b < nblocks; b += 256) {
+  // the same order as one load round per block row (v += row b for b = t, t + 256, ...), with
+  // up to four rows' loads in flight before their sums (1 round at <= 1024 rows instead of 4)
+  for (int b0 = threadIdx.x; b0 < nblocks; b0 += 4 * 256) {
+    double x[4][NV];
 #pragma unroll
-    for (int i = 0; i < NV; ++i) v[i] += partial[(long long)i * nblocks + b];
+    for (int u = 0; u < 4; ++u) {
+      const int b = b0 + u * 256 < nblocks ? b0 + u * 256 : b0;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) x[u][i] = partial[(long long)i * nblocks + b];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (b0 + u * 256 < nblocks) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) v[i] += x[u][i];
+      }
   }
   __shared__ double red[4][NV];
   __shared__ double G[NV];
@@ -2354,7 +2388,7 @@ static int fbg_nb(int resident, int nrows) {
 #define FBM_CASES(M) M(9) M(10) M(11) M(12) M(13) M(14) M(15) M(16)
 
 int launch_gemm_nn_gram(hipStream_t s, MvDesc A, int L, const double *M, int ldm, MvDesc X, int nrows,
-                        double *partial) {
+                        double *partial, const NngPro &pro) {
   const int k = X.ncols;
   if (k < 2 || k > 8 || L < 0 || L > 1024) throw Error(MIGMRES_EINVAL, "gemm_nn_gram: 2 <= k <= 8 and L <= 1024");
   const size_t lds = sizeof(double) * (size_t)(L > 0 ? L : 1) * k;
@@ -2365,7 +2399,7 @@ int launch_gemm_nn_gram(hipStream_t s, MvDesc A, int L, const double *M, int ldm
   case K:                                                                        \
     if (!occ[K][L]) occ[K][L] = fbg_resident(k_gemm_nn_gram<K>, lds);           \
     nb = fbg_nb(occ[K][L], nrows);                                               \
-    k_gemm_nn_gram<K><<<nb, FBG_NT, lds, s>>>(A, L, M, ldm, X, nrows, partial); \
+    k_gemm_nn_gram<K><<<nb, FBG_NT, lds, s>>>(A, L, M, ldm, X, nrows, partial, pro); \
     break;
     FBG_CASES(NNG_CASE)
 #undef NNG_CASE

@@ -220,6 +220,9 @@ void launch_abs(hipStream_t s, MvDesc Y, int nrows);  // Y = |Y| (negative entri
 // Import exchange layout [neighbour][column][count] (grp[i] = (offset, count) of entry i's
 // neighbour group): send[off*k + c*cnt + i-off] = X[lids[i], c]; ghost[c*ldg + i] = recv[...].
 void launch_pack(hipStream_t s, MvDesc X, const int *lids, const int2 *grp, int count, double *send, int k);
+// transposed apply: T[lids[i]] += recv[c * count + i] (one neighbour's contributions); Y = alpha T + beta Y
+void launch_export_add(hipStream_t s, MvDesc T, const int *lids, int count, int k, const double *recv);
+void launch_combine(hipStream_t s, MvDesc T, MvDesc Y, int nrows, double alpha, double beta);
 void launch_unpack(hipStream_t s, const double *recv, const int2 *grp, int count, int k, double *ghost,
                    long long ldg);
 

@@ -2041,35 +2041,46 @@ __global__ __launch_bounds__(256) void k_reduce(const double *__restrict__ parti
   if (s == 0 && o < nout) out[o] = alpha * ((red[0][l] + red[1][l]) + (red[2][l] + red[3][l]));
 }
 
-__global__ __launch_bounds__(256) void k_reduce_ld(const double *__restrict__ partial, int nblocks,
-                                                   int rows, int nout, int ldo, double alpha,
-                                                   double *__restrict__ out) {
-  __shared__ double red[4][64];
+// Partials of nblocks workgroups (block-major: partial[b * nout + o]) summed per output in a
+// fixed order: 64 outputs per workgroup and 16 slices (b = s mod 16), each slice with 8 loads in
+// flight into 4 running sums, then a fixed tree over the slices.  The 16 x 8 loads in flight
+// per output column make it 4 dependent rounds at 512 partial rows (the 4-slice form took 32:
+// 14.8 us per launch at 128^3, more than the 2 MB it reads).
+constexpr int RLD_S = 16;
+__global__ __launch_bounds__(64 * RLD_S) void k_reduce_ld(const double *__restrict__ partial, int nblocks,
+                                                          int rows, int nout, int ldo, double alpha,
+                                                          double *__restrict__ out) {
+  __shared__ double red[RLD_S][64];
   const int l = threadIdx.x & 63, s = threadIdx.x >> 6;
   const int o = blockIdx.x * 64 + l;
-  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  double a[4] = {0.0, 0.0, 0.0, 0.0};
   if (o < nout) {
     int b = s;
-    for (; b + 12 < nblocks; b += 16) {
-      a0 += partial[(long long)b * nout + o];
-      a1 += partial[(long long)(b + 4) * nout + o];
-      a2 += partial[(long long)(b + 8) * nout + o];
-      a3 += partial[(long long)(b + 12) * nout + o];
+    for (; b + 7 * RLD_S < nblocks; b += 8 * RLD_S) {
+      double x[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = partial[(long long)(b + j * RLD_S) * nout + o];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j & 3] += x[j];
     }
-    for (; b < nblocks; b += 4) a0 += partial[(long long)b * nout + o];
+    for (int j = 0; b < nblocks; b += RLD_S, ++j) a[j & 3] += partial[(long long)b * nout + o];
   }
-  red[s][l] = (a0 + a1) + (a2 + a3);
+  red[s][l] = (a[0] + a[1]) + (a[2] + a[3]);
   __syncthreads();
+#pragma unroll
+  for (int h = RLD_S / 2; h > 0; h >>= 1) {
+    if (s < h) red[s][l] = red[s][l] + red[s + h][l];
+    __syncthreads();
+  }
   if (s == 0 && o < nout)
-    out[(o % rows) + (long long)(o / rows) * ldo] =
-        alpha * ((red[0][l] + red[1][l]) + (red[2][l] + red[3][l]));
+    out[(o % rows) + (long long)(o / rows) * ldo] = alpha * red[0][l];
 }
 
 void launch_reduce_partials_ld(hipStream_t s, const double *partial, int nblocks, int rows, int cols,
                                int ldo, double alpha, double *out) {
   const int nout = rows * cols;
   if (nout <= 0) return;
-  k_reduce_ld<<<cdiv(nout, 64), 256, 0, s>>>(partial, nblocks, rows, nout, ldo, alpha, out);
+  k_reduce_ld<<<cdiv(nout, 64), 64 * RLD_S, 0, s>>>(partial, nblocks, rows, nout, ldo, alpha, out);
   LAUNCH_CHECK();
 }
 
@@ -2567,6 +2578,42 @@ void launch_unpack(hipStream_t s, const double *recv, const int2 *grp, int count
                    long long ldg) {
   if (count <= 0 || k <= 0) return;
   k_unpack<<<dim3(cdiv(count, 256), k), 256, 0, s>>>(recv, grp, count, k, ghost, ldg);
+  LAUNCH_CHECK();
+}
+
+// Reverse exchange of the transposed apply (Y = alpha A^T X + beta Y): the contributions one
+// neighbour computed for rows this rank owns, in the pack layout [column][count], added to
+// rows lids[0 .. count) (distinct within one neighbour's list), neighbour after neighbour.
+__global__ __launch_bounds__(256) void k_export_add(MvDesc T, const int *__restrict__ lids, int count,
+                                                    const double *__restrict__ recv) {
+#pragma clang fp contract(off)
+  const int c = blockIdx.y;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= count) return;
+  double *p = colp(T, c) + lids[i];
+  *p = *p + recv[(long long)c * count + i];
+}
+void launch_export_add(hipStream_t s, MvDesc T, const int *lids, int count, int k, const double *recv) {
+  if (count <= 0 || k <= 0) return;
+  k_export_add<<<dim3(cdiv(count, 256), k), 256, 0, s>>>(T, lids, count, recv);
+  LAUNCH_CHECK();
+}
+// Y = alpha T + beta Y with k_spmm's output rule (beta == 0 ignores Y)
+__global__ __launch_bounds__(256) void k_combine(MvDesc T, MvDesc Y, int nrows, double alpha, double beta) {
+#pragma clang fp contract(off)
+  const int c = blockIdx.y;
+  const long long r = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (r >= nrows) return;
+  const double t = colp(T, c)[r];
+  double *yp = colp(Y, c) + r;
+  if (beta == 0.0)
+    *yp = (alpha == 1.0) ? t : alpha * t;
+  else
+    *yp = alpha * t + beta * (*yp);
+}
+void launch_combine(hipStream_t s, MvDesc T, MvDesc Y, int nrows, double alpha, double beta) {
+  if (nrows <= 0 || Y.ncols <= 0) return;
+  k_combine<<<dim3(cdiv(nrows, 256), Y.ncols), 256, 0, s>>>(T, Y, nrows, alpha, beta);
   LAUNCH_CHECK();
 }
 

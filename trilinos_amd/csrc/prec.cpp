@@ -26,21 +26,6 @@ namespace migmres {
 // Y = M X.  Zero starting solution: the first sweep is Y = (omega d^-1) X; every further
 // sweep forms R = X - A Y (SpMM with alpha = -1, beta = 1 on a copy of X: y - sum, the
 // Tpetra::Details::residual expression) and Y = 1*Y + (omega d^-1) R.
-// Do any columns of X and Y share memory?  (Ifpack2 compares the data pointers,
-// Ifpack2_Relaxation_def.hpp:543-551; a column-range overlap test also catches views that
-// start at different columns of one block.)
-static bool mv_overlap(const migmres_mv &X, const migmres_mv &Y) {
-  if (X.ncols == 0 || Y.ncols == 0 || X.n_local == 0) return false;
-  for (int i = 0; i < X.ncols; ++i) {
-    const double *a0 = X.base + X.col_offset(i), *a1 = a0 + X.n_local;
-    for (int j = 0; j < Y.ncols; ++j) {
-      const double *b0 = Y.base + Y.col_offset(j), *b1 = b0 + Y.n_local;
-      if (a0 < b1 && b0 < a1) return true;
-    }
-  }
-  return false;
-}
-
 // scratch multivector with X's shape, (re)made when the column count changes
 static migmres_mv &scratch(migmres_mv *&w, const migmres_mv &X) {
   if (!w || w->ncols != X.ncols) {
@@ -178,6 +163,11 @@ static void chebyshev_compute(migmres_prec &M) {
 
 void prec_apply(migmres_prec &M, const migmres_mv &X_in, migmres_mv &Y) {
   MIG_CHECK(X_in.ncols == Y.ncols, "preconditioner apply: X and Y column counts differ");
+  if (M.kind == 2) {  // a user operator as the preconditioner
+    op_apply(*M.uop, X_in, Y);
+    ++M.n_apply;
+    return;
+  }
   MIG_CHECK(X_in.n_local == M.A->n_local && Y.n_local == M.A->n_local, "preconditioner apply: row map mismatch");
   migmres_ctx *c = M.ctx;
   const int n = M.A->n_local;
@@ -348,6 +338,7 @@ extern "C" int migmres_prec_apply(migmres_prec *M, const migmres_mv *X, migmres_
 extern "C" int migmres_prec_diagonal(const migmres_prec *M, double *dinv_out) {
   return guard([&] {
     MIG_CHECK(M && dinv_out, "prec_diagonal: null argument");
+    MIG_CHECK(M->kind != 2, "prec_diagonal: a user operator has no diagonal");
     MIG_HIP(hipMemcpy(dinv_out, M->d_dinv, sizeof(double) * M->A->n_local, hipMemcpyDeviceToHost));
   });
 }

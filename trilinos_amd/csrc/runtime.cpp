@@ -467,7 +467,11 @@ migmres_mv *mv_create(migmres_ctx *ctx, long long n_global, int n_local, int nco
   // that columns are not a power-of-two distance apart: with ld = 2^24 every column's row r
   // fell on the same HBM channel, and k_gemm_tn ran at 5.4 instead of 5.8-7.5 TB/s
   // (tools/mb_lib.cpp, 256^3).
-  m->ld = round_up(n_local > 0 ? n_local : 1, 64) + 64;
+  static const long long ld_pad = [] {
+    const char *e = std::getenv("MIGMRES_LD_PAD");  // rows; tuning only
+    return e ? std::atoll(e) : 64LL;
+  }();
+  m->ld = round_up(n_local > 0 ? n_local : 1, 64) + ld_pad;
   m->owner = true;
   const size_t bytes = (size_t)m->ld * (size_t)(ncols > 0 ? ncols : 1) * sizeof(double) + 256;
   try {
@@ -716,6 +720,9 @@ migmres_crs::~migmres_crs() {
   for (void *p : {(void *)d_rowptr, (void *)d_cols, (void *)d_export, (void *)d_vals, (void *)d_send,
                   (void *)d_ghost, (void *)d_psv, (void *)d_psk, (void *)d_psm, (void *)d_sel_int,
                   (void *)d_sel_bnd})
+    if (p) hipFree(p);
+  for (void *p : {(void *)d_trowptr, (void *)d_tcols, (void *)d_tiota, (void *)d_tvals, (void *)d_tbuf,
+                  (void *)d_tsend, (void *)d_trecv})
     if (p) hipFree(p);
 }
 
@@ -1363,11 +1370,101 @@ void crs_apply(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, double alpha,
   crs_apply_impl(A, X, Y, alpha, beta, ColScale{});
 }
 
+void op_apply(migmres_op &op, const migmres_mv &X, migmres_mv &Y) {
+  if (op.crs) {
+    crs_apply(*op.crs, X, Y, 1.0, 0.0);
+    return;
+  }
+  MIG_CHECK(X.n_local == op.n_local && Y.n_local == op.n_local, "user operator apply: row map mismatch");
+  MIG_CHECK(X.ncols == Y.ncols, "user operator apply: X and Y column counts differ");
+  const int rc = op.fn(op.user, &X, &Y);
+  if (rc != 0)
+    throw Error(MIGMRES_EOP, "user operator apply returned " + std::to_string(rc) + " (last error: " +
+                                 migmres_last_error() + ")");
+}
+
 // Y = A (M X) for the one-sweep right Jacobi M = omega D^-1 in one SpMM: every kernel forms
 // the operand (omega d^-1)_col x_col in registers, exactly as k_jacobi forms M X
 // (Ifpack2_Relaxation_def.hpp:1401-1425), so the result equals Jacobi pass + SpMM bit for bit.
 // Under a halo the exchange carries X itself; ghost columns take the owner's omega d^-1,
 // imported once by prec_import_ghost_scale.
+// Do any columns of X and Y share memory?  (Ifpack2 compares the data pointers,
+// Ifpack2_Relaxation_def.hpp:543-551; a column-range overlap test also catches views that
+// start at different columns of one block.)
+bool mv_overlap(const migmres_mv &X, const migmres_mv &Y) {
+  if (X.ncols == 0 || Y.ncols == 0 || X.n_local == 0) return false;
+  for (int i = 0; i < X.ncols; ++i) {
+    const double *a0 = X.base + X.col_offset(i), *a1 = a0 + X.n_local;
+    for (int j = 0; j < Y.ncols; ++j) {
+      const double *b0 = Y.base + Y.col_offset(j), *b1 = b0 + Y.n_local;
+      if (a0 < b1 && b0 < a1) return true;
+    }
+  }
+  return false;
+}
+
+void crs_apply_trans(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, double alpha, double beta) {
+  migmres_ctx *c = A.ctx;
+  MIG_CHECK(X.n_local == A.n_local && Y.n_local == A.n_local, "CRS apply (transpose): row map mismatch");
+  MIG_CHECK(X.ncols == Y.ncols, "CRS apply (transpose): X and Y column counts differ");
+  MIG_CHECK(!mv_overlap(X, Y), "CRS apply (transpose): X and Y may not alias one another");
+  const int k = X.ncols;
+  const int n_remote = (int)A.plan.remote_lids.size();
+  const int n_export = (int)A.export_lids.size();
+  const int n_out = A.n_local + n_remote;
+  if (k == 0) return;
+  if (!A.d_trowptr) {
+    const DevCsr dc{A.n_local, A.nnz, A.d_rowptr, A.d_cols, A.d_vals};
+    DevTrans t;
+    dev_transpose(c->stream, dc, n_out, t);
+    A.d_trowptr = t.rowptr;
+    A.d_tcols = t.cols;
+    A.d_tvals = t.vals;
+  }
+  const bool halo = c->dist && (n_remote > 0 || n_export > 0);
+  ProfScope ps(c, K_SPMM, 12.0 * A.nnz + 4.0 * (n_out + 1) + 8.0 * A.n_local * k * (beta == 0.0 ? 2.0 : 3.0));
+  if (!halo) {  // every column of A is owned: the transpose's rows are Y's rows
+    launch_spmm(c->stream, 0, A.n_local, A.d_trowptr, A.d_tcols, A.d_tvals, X.desc(), A.n_local, nullptr, 0,
+                Y.desc(), alpha, beta, nullptr, 0, ColScale{});
+    return;
+  }
+  if (k > A.tr_k) {
+    MIG_HIP(hipStreamSynchronize(c->stream));
+    for (double *p : {A.d_tbuf, A.d_tsend, A.d_trecv})
+      if (p) hipFree(p);
+    A.ld_t = ((long long)n_out + 63) / 64 * 64;
+    MIG_HIP(hipMalloc(&A.d_tbuf, sizeof(double) * ((size_t)A.ld_t * k + 2)));
+    MIG_HIP(hipMemset(A.d_tbuf, 0, sizeof(double) * ((size_t)A.ld_t * k + 2)));
+    MIG_HIP(hipMalloc(&A.d_tsend, sizeof(double) * ((size_t)n_remote * k + 1)));
+    MIG_HIP(hipMalloc(&A.d_trecv, sizeof(double) * ((size_t)n_export * k + 1)));
+    if (!A.d_tiota) {
+      std::vector<int> iota((size_t)n_remote + 1);
+      for (int i = 0; i <= n_remote; ++i) iota[(size_t)i] = i;
+      MIG_HIP(hipMalloc(&A.d_tiota, sizeof(int) * iota.size()));
+      MIG_HIP(hipMemcpy(A.d_tiota, iota.data(), sizeof(int) * iota.size(), hipMemcpyHostToDevice));
+    }
+    A.tr_k = k;
+  }
+  // T = A^T X over owned and ghost columns (Epetra's column-map vector), the ghost rows packed
+  // per owner, one message per neighbour each way (the import's lists with the roles swapped),
+  // then each neighbour's contributions added to the owned rows, neighbours in ascending PID
+  // order (Epetra_Export, combine mode Add), and Y = alpha T + beta Y.
+  const MvDesc T{A.d_tbuf, A.ld_t, nullptr, k};
+  launch_spmm(c->stream, 0, n_out, A.d_trowptr, A.d_tcols, A.d_tvals, X.desc(), A.n_local, nullptr, 0, T, 1.0, 0.0,
+              nullptr, 0, ColScale{});
+  const MvDesc Tg{A.d_tbuf + A.n_local, A.ld_t, nullptr, k};
+  launch_pack(c->stream, Tg, A.d_tiota, A.d_remote_grp, n_remote, A.d_tsend, k);
+  c->p2p_begin(c->stream);
+  for (auto &nb : A.recv_nbrs)
+    c->p2p_send(A.d_tsend + (size_t)nb.offset * k, sizeof(double) * nb.count * k, nb.pid);
+  for (auto &nb : A.send_nbrs)
+    c->p2p_recv(A.d_trecv + (size_t)nb.offset * k, sizeof(double) * nb.count * k, nb.pid);
+  c->p2p_end();
+  for (auto &nb : A.send_nbrs)
+    launch_export_add(c->stream, T, A.d_export + nb.offset, nb.count, k, A.d_trecv + (size_t)nb.offset * k);
+  launch_combine(c->stream, T, Y.desc(), A.n_local, alpha, beta);
+}
+
 bool crs_apply_jacobi_fused(migmres_crs &A, const migmres_prec &M, const migmres_mv &X, migmres_mv &Y) {
   migmres_ctx *c = A.ctx;
   const int n_remote = (int)A.plan.remote_lids.size();
@@ -1652,6 +1749,52 @@ extern "C" int migmres_crs_import_plan(const migmres_crs *A, int *export_lids, i
 extern "C" int migmres_crs_apply(migmres_crs *A, const migmres_mv *X, migmres_mv *Y, double alpha,
                                  double beta) {
   return guard([&] { crs_apply(*A, *X, *Y, alpha, beta); });
+}
+extern "C" int migmres_crs_apply_mode(migmres_crs *A, const migmres_mv *X, migmres_mv *Y, int mode, double alpha,
+                                      double beta) {
+  return guard([&] {
+    MIG_CHECK(A && X && Y, "bad arguments");
+    if (mode == MIGMRES_NO_TRANS)
+      crs_apply(*A, *X, *Y, alpha, beta);
+    else if (mode == MIGMRES_TRANS || mode == MIGMRES_CONJ_TRANS)  // real scalars: CONJ_TRANS = TRANS
+      crs_apply_trans(*A, *X, *Y, alpha, beta);
+    else
+      throw Error(MIGMRES_EINVAL, "CRS apply: mode must be MIGMRES_NO_TRANS, MIGMRES_TRANS or MIGMRES_CONJ_TRANS");
+  });
+}
+
+extern "C" int migmres_op_create(migmres_ctx *ctx, long long n_global, int n_local, migmres_apply_fn fn, void *user,
+                                 migmres_op **out) {
+  return guard([&] {
+    MIG_CHECK(ctx && fn && out && n_local >= 0, "op_create: bad arguments");
+    auto *op = new migmres_op();
+    op->ctx = ctx;
+    op->n_global = n_global;
+    op->n_local = n_local;
+    op->fn = fn;
+    op->user = user;
+    *out = op;
+  });
+}
+extern "C" int migmres_op_from_crs(migmres_crs *A, migmres_op **out) {
+  return guard([&] {
+    MIG_CHECK(A && out, "op_from_crs: bad arguments");
+    auto *op = new migmres_op();
+    op->ctx = A->ctx;
+    op->n_global = A->n_global;
+    op->n_local = A->n_local;
+    op->crs = A;
+    *out = op;
+  });
+}
+extern "C" int migmres_op_apply(migmres_op *op, const migmres_mv *X, migmres_mv *Y) {
+  return guard([&] {
+    MIG_CHECK(op && X && Y, "op_apply: bad arguments");
+    op_apply(*op, *X, *Y);
+  });
+}
+extern "C" int migmres_op_destroy(migmres_op *op) {
+  return guard([&] { delete op; });
 }
 
 extern "C" int migmres_mv_create(migmres_ctx *ctx, long long n_global, int n_local, int ncols,

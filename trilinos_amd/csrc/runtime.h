@@ -193,7 +193,24 @@ struct migmres_crs {
   double *d_send = nullptr, *d_recv = nullptr, *d_ghost = nullptr;
   long long ldg = 0;  // ghost block leading dimension: n_remote rounded up to even, padding zero
   int halo_k = 0;
+  // A^T (transposed apply): the local transpose in GeneralMTM's order (dev_transpose), built on
+  // the first transposed apply; with a halo the product goes to d_tbuf (owned + ghost rows, leading
+  // dimension ld_t), whose ghost rows travel back to their owners (d_tsend -> d_trecv)
+  int *d_trowptr = nullptr, *d_tcols = nullptr, *d_tiota = nullptr;
+  double *d_tvals = nullptr, *d_tbuf = nullptr, *d_tsend = nullptr, *d_trecv = nullptr;
+  long long ld_t = 0;
+  int tr_k = 0;
   ~migmres_crs();
+};
+
+// An operator given by a host callback (migmres_op_create) or wrapping a CRS (op_from_crs).
+struct migmres_op {
+  migmres_ctx *ctx = nullptr;
+  long long n_global = 0;
+  int n_local = 0;
+  migmres_apply_fn fn = nullptr;
+  void *user = nullptr;
+  migmres_crs *crs = nullptr;  // borrowed
 };
 
 // Point-Jacobi preconditioner (Ifpack2::Relaxation "Jacobi"): Y = M X with `sweeps`
@@ -217,12 +234,16 @@ struct migmres_prec {
   migmres_chebyshev_params cheb{};
   double cheb_computed_lmax = 0.0, cheb_lmax = 0.0, cheb_lmin = 0.0, cheb_ratio = 0.0;
   migmres_mv *cheb_w = nullptr, *cheb_p = nullptr;  // W (and the textbook form's P)
+  migmres_op *uop = nullptr;  // kind 2: a user operator (borrowed; A is null)
+  int n_local() const { return uop ? uop->n_local : A->n_local; }
   ~migmres_prec();
 };
 
 namespace migmres {
 
 void prec_apply(migmres_prec &M, const migmres_mv &X, migmres_mv &Y);
+// Y = op(X): the CRS apply, or the user callback (a nonzero return throws MIGMRES_EOP)
+void op_apply(migmres_op &op, const migmres_mv &X, migmres_mv &Y);
 
 migmres_mv *mv_create(migmres_ctx *ctx, long long n_global, int n_local, int ncols);
 migmres_mv *mv_view(migmres_mv *parent, const int *idx, int n);
@@ -240,6 +261,8 @@ void mv_norm(const migmres_mv &A, double *out, int type);
 void mv_init(migmres_mv &Y, double alpha);
 void mv_random(migmres_mv &Y, unsigned int *seed);
 void mv_assign(const migmres_mv &A, migmres_mv &Y);
+// do any columns of X and Y share memory?
+bool mv_overlap(const migmres_mv &X, const migmres_mv &Y);
 
 migmres_crs *crs_create(migmres_ctx *ctx, long long n_global, long long first, int n_local,
                         const long long *rowptr, const long long *gcols, const double *vals);
@@ -252,6 +275,10 @@ void fill_complete_device(migmres_crs *A, const long long *d_rowptr, const long 
                           std::vector<long long> &rowptr, std::vector<int> &lcols, std::vector<double> &lvals);
 // Y = alpha*A*X + beta*Y including the halo import.
 void crs_apply(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, double alpha, double beta);
+// Y = alpha*A^T*X + beta*Y (Tpetra apply mode TRANS; Epetra Multiply(TransA = true) at alpha 1,
+// beta 0): GeneralMTM's scatter order per row, ghost-column contributions exported back to their
+// owners and added in ascending neighbour order.
+void crs_apply_trans(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, double alpha, double beta);
 // Right Jacobi fused into the operator: Y = A (M X) with M = Ifpack2 Jacobi, one sweep from
 // zero, formed operand by operand inside the template SpMM -- bit-identical to prec_apply
 // followed by crs_apply.  Only where every row pair is templated and no halo is needed;

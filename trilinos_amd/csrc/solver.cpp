@@ -594,6 +594,11 @@ struct FastIcgs {
     return gram_on && (!slow->dgks || (gram_dgks && slow->dep_tol == 1.0 / std::sqrt(2.0))) && slow->steps == 2 && k >= 2 && L >= 1 && L <= 1024 &&
            ((k <= 8 && L * k <= 7680) || (k > 8 && k <= 16));
   }
+  // MIGMRES_FOLD_SMALL=0: the state reset, blk_old and C1 + C2 as separate launches
+  bool fold_small = [] {
+    const char *e = std::getenv("MIGMRES_FOLD_SMALL");
+    return !(e && e[0] == '0');
+  }();
   bool gram_dgks = [] {
     const char *e = std::getenv("MIGMRES_FB_GRAM_DGKS");
     return !(e && e[0] == '0');
@@ -681,9 +686,9 @@ struct FastIcgs {
     if (k == 1 && slow->dgks) return slow->project_and_normalize(X, Q, C, ldc, B, ldb);
     ++calls;
     pend = Pending{};
-    launch_state_reset(ctx->stream, st, slow->blk_tol, slow->sing_tol, slow->dgks ? 1 : 0, slow->dep_tol);
     const MvDesc xd = X.desc(), qd = Q.desc();
     if (k == 1) {  // blkOrtho1, then MvDot and MvScale
+      launch_state_reset(ctx->stream, st, slow->blk_tol, slow->sing_tol, slow->dgks ? 1 : 0, slow->dep_tol);
       enqueue_k1(X, Q);
       fetch(L, 1);
       return result_k1(L, C, B);
@@ -700,19 +705,42 @@ struct FastIcgs {
       tn(xd, k, xd, k, R1 + L, L + k);
       allreduce(R1, (size_t)(L + k) * k);
     }
-    launch_blk_old(ctx->stream, st, R1, L + k, L, k);
+    // The state is first read by blk_old (or by the closing update's prologue, which then takes
+    // the reset, blk_old and the coefficient sum C1 + C2 in its workgroup 0: no kernel between
+    // the passes reads it).
     const bool x1 = nn_then_tn(qd, L, R1, L + k, xd, k, R2);
-    launch_add_coef(ctx->stream, R1, L + k, R2, L, Cout, L, L, k);
+    const bool gram = gram_ok(L, k);
+    const bool fold = gram && gram_fuse && k <= 8 && !x1 && fold_small;
+    if (!fold) {
+      launch_state_reset(ctx->stream, st, slow->blk_tol, slow->sing_tol, slow->dgks ? 1 : 0, slow->dep_tol);
+      launch_blk_old(ctx->stream, st, R1, L + k, L, k);
+      launch_add_coef(ctx->stream, R1, L + k, R2, L, Cout, L, L, k);
+    }
     // X2 = X1 - Q C2 (reference order) when X holds X1, else X - Q (C1 + C2)
     const double *M2 = x1 ? R2 : Cout;
-    const bool gram = gram_ok(L, k);
     if (gram) {
       gram_alloc();
       flush_pending();
       int nb1 = 0;
       {
         ProfScope ps(ctx, K_GEMM_NN_DOT, 8.0 * n_local * (L + 2.0 * k));
-        if (gram_fuse && k <= 8)
+        if (fold) {
+          NngPro pro;
+          pro.C1 = R1;
+          pro.ld1 = L + k;
+          pro.C2 = R2;
+          pro.ld2 = L;
+          pro.cout = Cout;
+          pro.ldo = L;
+          pro.st = st;
+          pro.G = R1;
+          pro.ldg = L + k;
+          pro.dgks = slow->dgks ? 1 : 0;
+          pro.blk_tol = slow->blk_tol;
+          pro.sing_tol = slow->sing_tol;
+          pro.dep_tol = slow->dep_tol;
+          nb1 = launch_gemm_nn_gram(ctx->stream, qd, L, nullptr, L, xd, n_local, gb.part, pro);
+        } else if (gram_fuse && k <= 8)
           nb1 = launch_gemm_nn_gram(ctx->stream, qd, L, M2, L, xd, n_local, gb.part);
         else
           launch_gemm_nn(ctx->stream, qd, L, M2, L, xd, n_local, -1.0, 1.0);
@@ -866,6 +894,7 @@ struct migmres_solver {
   migmres_ctx *ctx = nullptr;
   Params p;
   migmres_prec *left = nullptr, *right = nullptr;  // borrowed (setLeftPrec / setRightPrec)
+  std::unique_ptr<migmres_prec> uprec[2];  // wrappers of user-operator preconditioners (set_prec_op)
   Icgs ortho;
   FastIcgs fast;
   bool use_fast = true;
@@ -893,7 +922,8 @@ double since(Clock::time_point t0) { return std::chrono::duration<double>(Clock:
 // LinearProblem (BelosLinearProblem.hpp) with optional left/right preconditioners.
 struct Problem {
   migmres_solver *S;
-  migmres_crs *A;
+  migmres_crs *A;              // the operator as a CRS, or null when it is a user operator:
+  migmres_op *Aop = nullptr;   // y = op(x) through its callback
   migmres_mv *X, *B;
   migmres_prec *LP = nullptr, *RP = nullptr;
   MvPtr R0, PR0;  // PR0 empty: PR0 == R0 (no left preconditioner)
@@ -908,15 +938,24 @@ struct Problem {
     if (!tmp.p || tmp->ncols != k) tmp = clone(k);
     return *tmp;
   }
+  void op_raw(const migmres_mv &x, migmres_mv &y) {  // uncounted
+    if (A)
+      crs_apply(*A, x, y, 1.0, 0.0);
+    else
+      op_apply(*Aop, x, y);
+  }
   void op(const migmres_mv &x, migmres_mv &y) {  // OPT::Apply(A)
     auto t0 = Clock::now();
-    crs_apply(*A, x, y, 1.0, 0.0);
+    op_raw(x, y);
     ++S->n_apply;
     if (S->p.verbosity & 1) {
-      MIG_HIP(hipStreamSynchronize(A->ctx->stream));
+      MIG_HIP(hipStreamSynchronize(X->ctx->stream));
       S->t_spmm += since(t0);
     }
   }
+  // every operator is the library's own (CRS, Jacobi, Chebyshev): it may be re-applied to
+  // regenerate a block, or applied ahead of need
+  bool own_ops() const { return A && !(LP && LP->kind == 2) && !(RP && RP->kind == 2); }
   void prec(migmres_prec &M, const migmres_mv &x, migmres_mv &y) {
     prec_apply(M, x, y);
     ++S->n_prec;
@@ -938,7 +977,7 @@ struct Problem {
       // right Jacobi fused into the template SpMM where the operator allows it (one launch,
       // no M x round trip through HBM; same bits); MIGMRES_NO_FUSED_JACOBI=1 disables
       const auto t0 = Clock::now();
-      if (fuse_jacobi && crs_apply_jacobi_fused(*A, *RP, x, y)) {
+      if (fuse_jacobi && A && crs_apply_jacobi_fused(*A, *RP, x, y)) {
         ++RP->n_apply;
         ++S->n_prec;
         ++S->n_apply;
@@ -1388,7 +1427,7 @@ struct Engine {
     // the orthogonalisation fell back and changed the block; it is counted when used).
     bool spec_ready = false;
     const char *se = std::getenv("MIGMRES_SPEC_SPMM");
-    const bool spec_on = !(se && se[0] == '0') && !it.Z.p && !lp.LP && !lp.RP && !(S->p.verbosity & 1);
+    const bool spec_on = !(se && se[0] == '0') && !it.Z.p && !lp.LP && !lp.RP && lp.A && !(S->p.verbosity & 1);
     while (!check(it) && it.cur_dim + k <= search) {
       ++it.num_iters;
       ++S->n_block_iters;
@@ -1428,9 +1467,9 @@ struct Engine {
       // X = Op V_prev again, bit for bit, if the device ICGS has to restart from its input
       const std::function<void()> regen = [&] {
         if (Znext.p)
-          crs_apply(*lp.A, *Znext, *Vnext, 1.0, 0.0);
+          lp.op_raw(*Znext, *Vnext);
         else if (!lp.LP && !lp.RP)
-          crs_apply(*lp.A, *Vprev, *Vnext, 1.0, 0.0);
+          lp.op_raw(*Vprev, *Vnext);
         else {  // not counted: the reference copies its input instead
           const long long na = S->n_apply, np = S->n_prec;
           lp.apply(*Vprev, *Vnext);
@@ -1439,7 +1478,8 @@ struct Engine {
         }
       };
       const int rank = S->use_fast && S->fast.supports(k)
-                           ? S->fast.project_and_normalize(*Vnext, *Q, subH.data(), lcl, subH2.data(), k, &regen)
+                           ? S->fast.project_and_normalize(*Vnext, *Q, subH.data(), lcl, subH2.data(), k,
+                                                           lp.own_ops() ? &regen : nullptr)
                            : S->ortho.project_and_normalize(*Vnext, *Q, subH.data(), lcl, subH2.data(), k);
       S->t_ortho += since(t0);
       S->fast.before_wait = nullptr;
@@ -2238,12 +2278,14 @@ extern "C" int migmres_solver_set_user_conv_test(migmres_solver *s, migmres_stat
   });
 }
 
-extern "C" int migmres_solver_solve(migmres_solver *s, migmres_crs *A, migmres_mv *X,
-                                    const migmres_mv *B, int *converged) {
+static int solve_impl(migmres_solver *s, migmres_crs *A, migmres_op *Aop, migmres_mv *X, const migmres_mv *B,
+                      int *converged) {
   return guard([&] {
-    MIG_CHECK(s && A && X && B, "bad solve arguments");
+    MIG_CHECK(s && (A || Aop) && X && B, "bad solve arguments");
+    if (!A && Aop->crs) A = Aop->crs;
+    const int a_local = A ? A->n_local : Aop->n_local;
     MIG_CHECK(s->p.ortho == "ICGS" || s->p.ortho == "DGKS", "\"Orthogonalization\" must be \"ICGS\" or \"DGKS\"");
-    MIG_CHECK(X->ncols == B->ncols && X->n_local == A->n_local && B->n_local == A->n_local,
+    MIG_CHECK(X->ncols == B->ncols && X->n_local == a_local && B->n_local == a_local,
               "LinearProblem: inconsistent X/B/A shapes");
     s->history.clear();
     s->n_apply = s->n_explicit = s->n_restarts = s->n_block_iters = s->n_prec = s->n_deflations = 0;
@@ -2252,7 +2294,7 @@ extern "C" int migmres_solver_solve(migmres_solver *s, migmres_crs *A, migmres_m
     const double comm0 = s->ctx->comm_seconds;
     auto t0 = Clock::now();
     for (migmres_prec *M : {s->left, s->right})
-      MIG_CHECK(!M || M->A->n_local == A->n_local, "preconditioner and operator row maps differ");
+      MIG_CHECK(!M || M->n_local() == a_local, "preconditioner and operator row maps differ");
     bool ok;
     if (s->p.pseudo) {
       MIG_CHECK(s->p.def_quorum <= s->p.block_size,
@@ -2260,6 +2302,7 @@ extern "C" int migmres_solver_solve(migmres_solver *s, migmres_crs *A, migmres_m
       PseudoEngine E(s, s->p.tol, s->p.max_iters);
       E.lp.S = s;
       E.lp.A = A;
+      E.lp.Aop = A ? nullptr : Aop;
       E.lp.X = X;
       E.lp.B = const_cast<migmres_mv *>(B);
       E.lp.LP = s->left;
@@ -2271,6 +2314,7 @@ extern "C" int migmres_solver_solve(migmres_solver *s, migmres_crs *A, migmres_m
       Engine E(s, s->p.tol, s->p.max_iters);
       E.lp.S = s;
       E.lp.A = A;
+      E.lp.Aop = A ? nullptr : Aop;
       E.lp.X = X;
       E.lp.B = const_cast<migmres_mv *>(B);
       E.lp.LP = s->left;
@@ -2282,6 +2326,35 @@ extern "C" int migmres_solver_solve(migmres_solver *s, migmres_crs *A, migmres_m
     s->t_total = since(t0);
     s->t_comm = s->ctx->comm_seconds - comm0;
     if (converged) *converged = ok ? 1 : 0;
+  });
+}
+
+extern "C" int migmres_solver_solve(migmres_solver *s, migmres_crs *A, migmres_mv *X,
+                                    const migmres_mv *B, int *converged) {
+  if (!A) return guard([] { throw Error(MIGMRES_EINVAL, "bad solve arguments"); });
+  return solve_impl(s, A, nullptr, X, B, converged);
+}
+extern "C" int migmres_solver_solve_op(migmres_solver *s, migmres_op *A, migmres_mv *X, const migmres_mv *B,
+                                       int *converged) {
+  if (!A) return guard([] { throw Error(MIGMRES_EINVAL, "bad solve arguments"); });
+  return solve_impl(s, nullptr, A, X, B, converged);
+}
+extern "C" int migmres_solver_set_prec_op(migmres_solver *s, int side, migmres_op *M) {
+  return guard([&] {
+    MIG_CHECK(s, "set_prec_op: null solver");
+    MIG_CHECK(side == MIGMRES_LEFT_PREC || side == MIGMRES_RIGHT_PREC, "set_prec_op: side must be left (0) or right (1)");
+    std::unique_ptr<migmres_prec> &w = s->uprec[side == MIGMRES_LEFT_PREC ? 0 : 1];
+    migmres_prec *&slot = side == MIGMRES_LEFT_PREC ? s->left : s->right;
+    if (!M) {
+      if (slot == w.get()) slot = nullptr;
+      w.reset();
+      return;
+    }
+    w.reset(new migmres_prec());
+    w->ctx = M->ctx;
+    w->kind = 2;
+    w->uop = M;
+    slot = w.get();
   });
 }
 

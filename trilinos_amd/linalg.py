@@ -14,7 +14,7 @@ import os
 
 import numpy as np
 
-from ._lib import call, dptr, iptr, lptr, lib, MigmresError  # noqa: F401
+from ._lib import APPLY_FN, call, dptr, iptr, lptr, lib, MigmresError  # noqa: F401
 
 TWO_NORM, ONE_NORM, INF_NORM = 1, 0, 2
 
@@ -205,10 +205,20 @@ class CrsMatrix:
         return dict(export_lids=el[:self.n_export], export_pids=ep[:self.n_export],
                     remote_lids=rl[:self.n_remote], remote_pids=rp[:self.n_remote])
 
-    def apply(self, X, Y, alpha=1.0, beta=0.0):
-        """Y = alpha*A*X + beta*Y (Tpetra::CrsMatrix::apply, Tpetra_CrsMatrix_def.hpp:5176-5208;
-        with alpha=1, beta=0 this is Epetra_CrsMatrix::Multiply(false, X, Y))."""
-        call("migmres_crs_apply", self.h, X.h, Y.h, alpha, beta)
+    NO_TRANS, TRANS, CONJ_TRANS = 0, 1, 2  # Teuchos::ETransp
+
+    def apply(self, X, Y, alpha=1.0, beta=0.0, mode=0):
+        """Y = alpha*op(A)*X + beta*Y, op(A) = A or A^T by `mode` (Tpetra::CrsMatrix::apply,
+        Tpetra_CrsMatrix_def.hpp:5176-5208; with alpha=1, beta=0 this is
+        Epetra_CrsMatrix::Multiply(TransA, X, Y), Epetra_CrsMatrix.cpp:3107-3285)."""
+        if mode == self.NO_TRANS:
+            call("migmres_crs_apply", self.h, X.h, Y.h, alpha, beta)
+        else:
+            call("migmres_crs_apply_mode", self.h, X.h, Y.h, int(mode), alpha, beta)
+
+    def multiply(self, trans, X, Y):
+        """Epetra_CrsMatrix::Multiply(TransA, X, Y)."""
+        self.apply(X, Y, 1.0, 0.0, self.TRANS if trans else self.NO_TRANS)
 
     Apply = apply
 
@@ -227,12 +237,58 @@ class CrsMatrix:
             pass
 
 
+class Operator:
+    """A user operator: the analogue of an Epetra_Operator / Tpetra::Operator subclass handed to
+    Belos (BelosOperatorTraits.hpp:108-155), e.g. the Vector_Operator family of
+    belos/epetra/test/BlockGmres/test_bl_gmres_diag.cpp.  `apply(X, Y)` is a Python function of
+    two device MultiVectors (borrowed handles, valid during the call) that leaves Y = op(X) in the
+    context's stream order -- any trilinos_amd call on the same Comm does, nested solves included.
+    Usable as the solver's operator (LinearProblem(A=Operator, ...)) and as a preconditioner."""
+
+    def __init__(self, comm, n_global, apply):
+        self.comm, self.n_global = comm, n_global
+        _, self.n_local = uniform_map(n_global, comm.nranks, comm.rank)
+        self._apply = apply
+        self.error = None
+        self._cb = APPLY_FN(self._trampoline)
+        h = C.c_void_p()
+        call("migmres_op_create", comm.h, n_global, self.n_local, self._cb, None, C.byref(h))
+        self.h = h
+
+    def _trampoline(self, _user, xh, yh):
+        try:
+            X = MultiVector(self.comm, self.n_global, 0, _handle=C.c_void_p(xh), _borrowed=True)
+            Y = MultiVector(self.comm, self.n_global, 0, _handle=C.c_void_p(yh), _borrowed=True)
+            self._apply(X, Y)
+            return 0
+        except BaseException as e:  # reported by the failing library call (MIGMRES_EOP)
+            self.error = e
+            return 1
+
+    def apply(self, X, Y):
+        call("migmres_op_apply", self.h, X.h, Y.h)
+
+    Apply = apply
+
+    def close(self):
+        if self.h:
+            call("migmres_op_destroy", self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class MultiVector:
     """Epetra_MultiVector-like block of `ncols` columns over the uniform row map."""
 
-    def __init__(self, comm, n_global, ncols, _handle=None, _parent=None):
+    def __init__(self, comm, n_global, ncols, _handle=None, _parent=None, _borrowed=False):
         self.comm = comm
         self._parent = _parent  # keeps the parent alive for views
+        self._borrowed = _borrowed  # a handle the library owns (user-operator callbacks)
         if _handle is None:
             _, n_local = uniform_map(n_global, comm.nranks, comm.rank)
             h = C.c_void_p()
@@ -275,9 +331,9 @@ class MultiVector:
         return s.value
 
     def close(self):
-        if self.h:
+        if self.h and not self._borrowed:
             call("migmres_mv_destroy", self.h)
-            self.h = None
+        self.h = None
 
     def __del__(self):
         try:
