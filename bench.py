@@ -123,7 +123,7 @@ def csr_spmm_forms(ta, comm, args, n, k, nnz, call, reps=20):
             if args.matrix == "FlanProxy":
                 A2 = ta.CrsMatrix.galeri(comm, "FlanProxy", 81, 81, 80)
             else:
-                A2 = ta.CrsMatrix.galeri(comm, args.matrix, args.nx, args.nx, args.nx)
+                A2 = ta.CrsMatrix.galeri(comm, args.matrix, args.nx, args.nx, args.nz if args.nz > 0 else args.nx)
         finally:
             for key, v in old.items():
                 if v is None:
@@ -227,6 +227,9 @@ def main():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=25)
     ap.add_argument("--nx", type=int, default=256)
+    ap.add_argument("--nz", type=int, default=0,
+                    help="planes of the Laplace3D / Brick3D grid (0: nx); e.g. --nz 32 gives one GPU the rows one "
+                         "rank of the 8-GPU 256^3 run holds")
     ap.add_argument("--k", type=int, default=8)
     ap.add_argument("--nb", type=int, default=25)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -299,8 +302,9 @@ def main():
         n = 3 * dims[0] * dims[1] * dims[2]
         A = ta.CrsMatrix.galeri(comm, "FlanProxy", *dims)
     else:
-        n = nx ** 3
-        A = ta.CrsMatrix.galeri(comm, args.matrix, nx, nx, nx)
+        nz = args.nz if args.nz > 0 else nx
+        n = nx * nx * nz
+        A = ta.CrsMatrix.galeri(comm, args.matrix, nx, nx, nz)
     M = None
     if args.prec != "none":
         if args.prec_type == "chebyshev":
@@ -374,10 +378,11 @@ def main():
     value = steps / elapsed
     model_bytes = iteration_bytes_model(n, nnz_total, k, nb, steps)
     headline = (args.solver == "BLOCK GMRES" and args.matrix == "Laplace3D" and args.prec == "none"
-                and args.ortho == "ICGS" and not args.matrix_file and nx == 256 and k == 8 and nb == 25)
+                and args.ortho == "ICGS" and not args.matrix_file and nx == 256 and args.nz in (0, 256) and k == 8
+                and nb == 25)
     mname = (os.path.basename(args.matrix_file) if args.matrix_file else
              f"FlanProxy n={n} (synthetic stand-in for SuiteSparse Flan_1565)" if args.matrix == "FlanProxy" else
-             f"{args.matrix} n={nx}^3")
+             f"{args.matrix} n={nx}^3" if args.nz in (0, nx) else f"{args.matrix} n={nx}x{nx}x{args.nz}")
     wl = (f"3-D 7-pt Laplacian n={nx}^3 fp64, k={k} RHS, Block GMRES Num Blocks {nb}, ICGS, fixed work (tol 0)"
           if headline else
           f"{mname} fp64, k={k} RHS, {args.solver} Num Blocks {nb}, {args.ortho}, " +

@@ -435,7 +435,10 @@ int migmres_solver_history(const migmres_solver *s, double *out, int *nrows, int
 /* Counters: [0] operator applies, [1] explicit residual checks, [2] restarts,
  * [3] blkOrthoSing fallbacks, [4] block iterations, [5] preconditioner applies,
  * [6] pseudo-block deflations, [7] findBasis calls taken in Gram form (CholQR2),
- * [8] of those handed back to the column passes by the pivot-ratio gate. */
+ * [8] of those handed back to the column passes (the pivot-ratio gate, or DGKS's criterion
+ * asking a second projection of some columns only), [9] DGKS blocks in which no column needed
+ * DGKS's second projection (CholQR1, B = R1: DGKS's single Gram-Schmidt pass per column),
+ * [10] DGKS blocks handed to the column passes because only some columns needed it. */
 int migmres_solver_counters(const migmres_solver *s, long long *out, int n);
 /* Seconds spent in named phases: [0] total solve, [1] SpMM, [2] orthogonalization,
  * [3] host least-squares, [4] communication, [5] status tests, [6] restarts, [7] setup.

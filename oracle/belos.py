@@ -987,4 +987,5 @@ def solve(A, B, params, X0=None, left=None, right=None):
     return dict(X=lp.X, converged=ok, iterations=sm.num_iters, achieved_tol=sm.achieved_tol,
                 loa=sm.loa, n_apply=lp.n_apply, n_prec=lp.n_prec, n_explicit=sm.conv.n_explicit,
                 restarts=sm.n_restarts_total, history=np.array(sm.stest.history),
-                blk_ortho_sing=sm.ortho.counters.get("blkOrthoSing", 0))
+                blk_ortho_sing=sm.ortho.counters.get("blkOrthoSing", 0),
+                fb_decisions={key: sm.ortho.counters.get(key, 0) for key in ("fb_single", "fb_double", "fb_mixed")})

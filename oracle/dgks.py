@@ -43,6 +43,7 @@ class DGKS(ICGS):
     def find_basis(self, X, B, complete_basis):
         """findBasis (BelosDGKSOrthoManager.hpp:1000-1243), howMany = all columns."""
         xc = X.shape[1]
+        twos = []  # per column j >= 1: did DGKS's criterion ask the second projection?
         for j in range(xc):
             Xj = X[:, j]
             prevX = X[:, :j]
@@ -56,7 +57,8 @@ class DGKS(ICGS):
                 product = _tn(prevX, Xj)
                 Xj -= prevX @ product
                 new_dot = _dot(Xj, Xj)
-                if math.sqrt(abs(new_dot)) < self.dep_tol * math.sqrt(abs(old_dot)):
+                twos.append(math.sqrt(abs(new_dot)) < self.dep_tol * math.sqrt(abs(old_dot)))
+                if twos[-1]:
                     P2 = _tn(prevX, Xj)
                     product = product + P2
                     Xj -= prevX @ P2
@@ -86,6 +88,11 @@ class DGKS(ICGS):
             B[j, j] = 0.0 if add_vec else diag
             if not add_vec:
                 B[:j, j] = product
+        if not complete_basis and xc > 1:
+            # the block's decision pattern (the device's Gram form takes one per block:
+            # tests/test_gpu_solver.py::test_dgks_gram_decisions_match_oracle)
+            key = "fb_single" if not any(twos) else "fb_double" if all(twos) else "fb_mixed"
+            self.counters[key] = self.counters.get(key, 0) + 1
         return xc
 
     def _blk_ortho_sing(self, X, Q, C, B):

@@ -85,6 +85,12 @@ def hist_close(h, ref, rerun=None, *, drift_ok=False, label=None):
                                 f"drift envelope {envelope[worst]:.3e}")
 
 
+def record_margin(kind, payload):
+    """A non-history record in the parity log (e.g. DGKS decision counts)."""
+    test = os.environ.get("PYTEST_CURRENT_TEST", "").rsplit(" (", 1)[0]
+    _log(dict({"test": test, "kind": kind}, **payload))
+
+
 def oracle_rerun(fn, *args, **kw):
     """A callable for hist_close: the oracle call fn(*args, **kw) (returning a result dict with
     "history") with its inner products summed in reverse row order."""

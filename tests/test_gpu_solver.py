@@ -19,7 +19,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-from tests.parity import hist_close as _hist_close, oracle_rerun  # noqa: F401 (re-exported)
+from tests.parity import hist_close as _hist_close, oracle_rerun, record_margin  # noqa: F401 (re-exported)
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
@@ -372,3 +372,30 @@ def test_one_rank_rccl_transport(monkeypatch):
     _hist_close(rccl[3], ref["history"], oracle_rerun(ob.solve, Aor.apply, Bh, params))
     np.testing.assert_allclose(rccl[4], plain[4], rtol=0, atol=1e-12 * np.abs(plain[4]).max())
     assert np.array_equal(rccl[5], [1.5, -2.0])
+
+
+@pytest.mark.parametrize("kind,dims,k,nb,seed", [("Laplace3D", (16, 16, 16), 8, 6, 3),
+                                                 ("Laplace2D", (40, 25, 1), 3, 20, 2),
+                                                 ("Laplace3D", (12, 12, 12), 12, 5, 4)])
+def test_dgks_gram_decisions_match_oracle(comm, kind, dims, k, nb, seed):
+    """DGKS's own criterion decides in the Gram form: per block the
+    device counts how many took no second projection (CholQR1), and how many had some columns
+    asking it (handed to the column passes); both equal the oracle's column-by-column DGKS
+    findBasis decisions on the same solve, and the solve follows the oracle within the strict
+    history bar.  Counters [9] / [10] (include/migmres.h)."""
+    from oracle import belos as ob, epetra as oe
+    params = {"Num Blocks": nb, "Block Size": k, "Maximum Iterations": 2000, "Maximum Restarts": 30,
+              "Convergence Tolerance": 1e-8, "Orthogonalization": "DGKS"}
+    sm, ret, X, B, Xex = _device_solve(comm, kind, dims, k, seed, params)
+    n, gen = _gen(kind, dims)
+    A = oe.DistCrs(gen, n, 1)
+    ref = ob.solve(A.apply, A.apply(Xex), params)
+    c = sm.counters()
+    d = ref["fb_decisions"]
+    assert sm.getNumIters() == ref["iterations"]
+    assert c["gram_dgks_single"] == d["fb_single"]
+    assert c["gram_dgks_mixed"] == d["fb_mixed"]
+    assert c["gram_calls"] - c["gram_skips"] - c["gram_dgks_single"] == d["fb_double"]
+    record_margin("dgks_gram_decisions", dict(device=dict(single=c["gram_dgks_single"], mixed=c["gram_dgks_mixed"],
+                                                          calls=c["gram_calls"], skips=c["gram_skips"]), oracle=d))
+    _hist_close(sm.residualHistory(), ref["history"], oracle_rerun(ob.solve, A.apply, A.apply(Xex), params))

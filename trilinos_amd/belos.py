@@ -375,10 +375,10 @@ class BlockGmresSolMgr:
         return out[:nr.value * nc.value].reshape(nr.value, nc.value)
 
     def counters(self):
-        out = (C.c_longlong * 9)()
-        call("migmres_solver_counters", self.h, out, 9)
+        out = (C.c_longlong * 11)()
+        call("migmres_solver_counters", self.h, out, 11)
         keys = ("applies", "explicit_checks", "restarts", "blk_ortho_sing", "block_iterations",
-                "prec_applies", "deflations", "gram_calls", "gram_skips")
+                "prec_applies", "deflations", "gram_calls", "gram_skips", "gram_dgks_single", "gram_dgks_mixed")
         return dict(zip(keys, list(out)))
 
     def timers(self):
@@ -389,7 +389,7 @@ class BlockGmresSolMgr:
 
     def __del__(self):
         try:
-            if self.h is not None:
+            if self.h is not None and (self.comm is None or self.comm.h):
                 call("migmres_solver_destroy", self.h)
         except Exception:
             pass

@@ -16,7 +16,10 @@ struct IcgsState {
   int dgks;    // 1: DGKSOrthoManager findBasis (second projection only under dep_tol)
   double dep_tol;
   int gram_skip;  // findBasis in Gram form handed the block back to the column passes
-  int gram_pad_;
+  // DGKS in Gram form: no column of the block took DGKS's second projection (its criterion on
+  // the first pass's pivots): CholQR1, B = R1 (gram_single); some but not all did: the column
+  // passes decide column by column (gram_mixed, with gram_skip)
+  int gram_single, gram_mixed, gram_pad_;
 };
 
 // findBasis in Gram form (icgs.hip; ICGS with two passes, 2 <= k <= 16).  The partial-writing
@@ -38,6 +41,7 @@ struct NngPro {
   const double *G = nullptr;
   int ldg = 0, dgks = 0;
   double blk_tol = 0.0, sing_tol = 0.0, dep_tol = 0.0;
+  int contig = 0;  // (tuning) row order of the pass: 0 grid-stride, 1 contiguous range per workgroup
 };
 int launch_gemm_nn_gram(hipStream_t s, MvDesc A, int L, const double *M, int ldm, MvDesc X, int nrows,
                         double *partial, const NngPro &pro = NngPro());

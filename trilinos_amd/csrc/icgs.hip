@@ -1960,8 +1960,17 @@ __global__ __launch_bounds__(FBG_NT) void k_gemm_nn_gram(MvDesc A, int L, const 
   double g[NV];
 #pragma unroll
   for (int i = 0; i < NV; ++i) g[i] = 0.0;
-  for (long long r = 2LL * ((long long)blockIdx.x * FBG_NT + threadIdx.x); r < nrows;
-       r += 2LL * gridDim.x * FBG_NT) {
+  // row pairs grid-stride (the resident grid sweeps one band at a time), or (pro.contig)
+  // workgroup b streams its own contiguous range of 512-row steps
+  long long rb = 2LL * ((long long)blockIdx.x * FBG_NT + threadIdx.x), re = nrows, rs = 2LL * gridDim.x * FBG_NT;
+  if (pro.contig) {
+    const long long nst = ((long long)nrows + 2 * FBG_NT - 1) / (2 * FBG_NT);
+    rb = (nst * blockIdx.x / gridDim.x) * 2 * FBG_NT + 2 * threadIdx.x;
+    re = (nst * (blockIdx.x + 1) / gridDim.x) * 2 * FBG_NT;
+    re = re < nrows ? re : nrows;
+    rs = 2 * FBG_NT;
+  }
+  for (long long r = rb; r < re; r += rs) {
     d2 acc[K];
 #pragma unroll
     for (int c = 0; c < K; ++c) acc[c] = d2{0.0, 0.0};
@@ -2012,7 +2021,7 @@ __global__ __launch_bounds__(FBG_NT) void k_fbg_gram(MvDesc X, int nrows, double
 template <int K>
 __global__ __launch_bounds__(FBG_NT) void k_fbg_a(MvDesc X, int nrows, const IcgsState *__restrict__ st,
                                                  const double *__restrict__ w, double *__restrict__ partial, int rev) {
-  if (st->gram_skip) return;
+  if (st->gram_skip || st->gram_single) return;
   __shared__ double T1[16 * K];
   for (int e = threadIdx.x; e < 16 * K; e += FBG_NT) T1[e] = w[e];
   __syncthreads();
@@ -2036,6 +2045,7 @@ template <int K>
 __global__ __launch_bounds__(FBG_NT) void k_fbg_b(MvDesc X, int nrows, const IcgsState *__restrict__ st,
                                                  const double *__restrict__ w, int rev) {
   if (st->gram_skip) return;
+  const bool single = st->gram_single != 0;  // DGKS CholQR1: X T1 only
   __shared__ double T1[16 * K], T2[16 * K];
   for (int e = threadIdx.x; e < 16 * K; e += FBG_NT) {
     T1[e] = w[e];
@@ -2049,7 +2059,7 @@ __global__ __launch_bounds__(FBG_NT) void k_fbg_b(MvDesc X, int nrows, const Icg
 #pragma unroll
     for (int c = 0; c < K; ++c) x[c] = *(const d2 *)(colp_(X, c) + r);
     fbg_apply<K>(x, T1);
-    fbg_apply<K>(x, T2);
+    if (!single) fbg_apply<K>(x, T2);
     const bool two = r + 1 < nrows;
 #pragma unroll
     for (int c = 0; c < K; ++c) st_pair(colp_(X, c) + r, x[c].x, x[c].y, two);
@@ -2102,7 +2112,7 @@ template <int K, bool APPLY>
 __global__ __launch_bounds__(FBG_NT) void k_fbg_gram_m(MvDesc X, int nrows, const IcgsState *__restrict__ st,
                                                       const double *__restrict__ w, double *__restrict__ partial,
                                                       int rev) {
-  if (APPLY && st->gram_skip) return;
+  if (APPLY && (st->gram_skip || st->gram_single)) return;
   constexpr int NV = K * (K + 1) / 2, NW = FBG_NT / 64;
   __shared__ __attribute__((aligned(16))) double tile[NW][16 * FBM_S];
   __shared__ double red[NW][NV];
@@ -2155,6 +2165,7 @@ template <int K>
 __global__ __launch_bounds__(FBG_NT) void k_fbg_b_m(MvDesc X, int nrows, const IcgsState *__restrict__ st,
                                                    const double *__restrict__ w, int rev) {
   if (st->gram_skip) return;
+  const bool single = st->gram_single != 0;  // DGKS CholQR1: X T1 only
   constexpr int NW = FBG_NT / 64;
   const int l = threadIdx.x & 63, wv = threadIdx.x >> 6, lr = l & 15;
   double a1[4], a2[4];
@@ -2174,7 +2185,7 @@ __global__ __launch_bounds__(FBG_NT) void k_fbg_b_m(MvDesc X, int nrows, const I
     for (int g = 0; g < 4; ++g) {
       const d4 y = fbm_mul(a1, xv[g]);
       double yb[4] = {y[0], y[1], y[2], y[3]};
-      const d4 z = fbm_mul(a2, yb);
+      const d4 z = single ? y : fbm_mul(a2, yb);
       const long long r = r0 + 16 * g + lr;
       if (r < nrows) {
 #pragma unroll
@@ -2191,14 +2202,16 @@ __global__ __launch_bounds__(FBG_NT) void k_fbg_b_m(MvDesc X, int nrows, const I
 __global__ __launch_bounds__(256) void k_fbg_chol_l(const double *__restrict__ gsum, int k, int stage,
                                                    IcgsState *st, double *__restrict__ w, double gate) {
   __shared__ double g[136], R[16][17], T[16][17];
-  __shared__ int ok;
+  __shared__ int ok, any2, all2;
   const int t = threadIdx.x, nv = k * (k + 1) / 2;
   if (t < nv) g[t] = gsum[t];
-  if (t == 0) ok = 1;
+  if (t == 0) ok = 1, any2 = 0, all2 = 1;
   __syncthreads();
-  if (stage == 2 && st->gram_skip) return;
+  if (stage == 2 && (st->gram_skip || st->gram_single)) return;
   if (stage == 1 && t == 0) {
     st->gram_skip = 0;
+    st->gram_single = 0;
+    st->gram_mixed = 0;
     bool dep = false;
     for (int c = 0; c < k; ++c) dep = dep || fabs(g[c * (c + 1) / 2 + c]) < fabs(st->blk_old[c] * st->blk_tol);
     if (dep) st->dep = 1.0;
@@ -2209,6 +2222,11 @@ __global__ __launch_bounds__(256) void k_fbg_chol_l(const double *__restrict__ g
       double s = gjj;
       for (int i = 0; i < j; ++i) s -= R[i][j] * R[i][j];
       if (!(gjj > 0.0 && s >= gate * gjj)) ok = 0;
+      if (j > 0) {  // DGKS findBasis: a second projection iff sqrt|newDot| < dep_tol sqrt|oldDot|
+        const bool two = sqrt(fabs(s)) < st->dep_tol * sqrt(fabs(gjj));
+        any2 |= two;
+        all2 &= two;
+      }
       R[j][j] = sqrt(fabs(s));
     }
     __syncthreads();
@@ -2222,6 +2240,19 @@ __global__ __launch_bounds__(256) void k_fbg_chol_l(const double *__restrict__ g
   if (!ok) {
     if (t == 0) st->gram_skip = 1;
     return;
+  }
+  const bool dgks = stage == 1 && st->dgks;
+  if (dgks && any2 && !all2) {  // DGKS re-projects some columns only: the column passes
+    if (t == 0) st->gram_skip = st->gram_mixed = 1;
+    return;
+  }
+  const bool single = dgks && !any2;  // DGKS: one projection per column = CholQR1, B = R1
+  if (single && t == 0) st->gram_single = 1;
+  if (single && t < nv) {
+    int c = 0;
+    while ((c + 1) * (c + 2) / 2 <= t) ++c;
+    const int i = t - c * (c + 1) / 2;
+    st->B[i + 16 * c] = R[i][c];
   }
   if (t < k) {  // column t of T = R^{-1}
     const int c = t;
@@ -2292,12 +2323,14 @@ __global__ __launch_bounds__(256) void k_fbg_chol(const double *__restrict__ par
   }
   __syncthreads();
   if (stage == 0 || threadIdx.x != 0) return;
-  if (stage == 2 && st->gram_skip) return;
+  if (stage == 2 && (st->gram_skip || st->gram_single)) return;
   double g[NV];
 #pragma unroll
   for (int i = 0; i < NV; ++i) g[i] = G[i];
   if (stage == 1) {
     st->gram_skip = 0;
+    st->gram_single = 0;
+    st->gram_mixed = 0;
     bool dep = false;
 #pragma unroll
     for (int c = 0; c < K; ++c) dep = dep || fabs(g[c * (c + 1) / 2 + c]) < fabs(st->blk_old[c] * st->blk_tol);
@@ -2305,7 +2338,8 @@ __global__ __launch_bounds__(256) void k_fbg_chol(const double *__restrict__ par
   }
   // G = R^T R, R upper triangular with a positive diagonal; pivot ratios against the gate
   double R[K][K], T[K][K];
-  bool ok = true;
+  bool ok = true, any2 = false, all2 = true;
+  const double dep_tol = st->dep_tol;
 #pragma unroll
   for (int j = 0; j < K; ++j) {
     const double gjj = g[j * (j + 1) / 2 + j];
@@ -2313,6 +2347,11 @@ __global__ __launch_bounds__(256) void k_fbg_chol(const double *__restrict__ par
 #pragma unroll
     for (int i = 0; i < j; ++i) s -= R[i][j] * R[i][j];
     ok = ok && gjj > 0.0 && s >= gate * gjj;
+    if (j > 0) {  // DGKS findBasis: a second projection iff sqrt|newDot| < dep_tol sqrt|oldDot|
+      const bool two = sqrt(fabs(s)) < dep_tol * sqrt(fabs(gjj));
+      any2 = any2 || two;
+      all2 = all2 && two;
+    }
     const double d = sqrt(fabs(s));
     R[j][j] = d;
 #pragma unroll
@@ -2326,6 +2365,20 @@ __global__ __launch_bounds__(256) void k_fbg_chol(const double *__restrict__ par
   if (!ok) {
     st->gram_skip = 1;
     return;
+  }
+  const bool dgks = stage == 1 && st->dgks;
+  if (dgks && any2 && !all2) {  // DGKS re-projects some columns only: the column passes
+    st->gram_skip = 1;
+    st->gram_mixed = 1;
+    return;
+  }
+  const bool single = dgks && !any2;  // DGKS: one projection per column = CholQR1, B = R1
+  if (single) {
+    st->gram_single = 1;
+#pragma unroll
+    for (int c = 0; c < K; ++c)
+#pragma unroll
+      for (int i = 0; i <= c; ++i) st->B[i + 16 * c] = R[i][c];
   }
   // T = R^{-1}
 #pragma unroll
@@ -2392,6 +2445,12 @@ int launch_gemm_nn_gram(hipStream_t s, MvDesc A, int L, const double *M, int ldm
   const int k = X.ncols;
   if (k < 2 || k > 8 || L < 0 || L > 1024) throw Error(MIGMRES_EINVAL, "gemm_nn_gram: 2 <= k <= 8 and L <= 1024");
   const size_t lds = sizeof(double) * (size_t)(L > 0 ? L : 1) * k;
+  static const int contig = [] {  // MIGMRES_NNG_CONTIG=1: contiguous row range per workgroup
+    const char *e = std::getenv("MIGMRES_NNG_CONTIG");
+    return e ? std::atoi(e) : 0;
+  }();
+  NngPro pr = pro;
+  pr.contig = contig;
   static int occ[9][1025];
   int nb = 1;
   switch (k) {
@@ -2399,7 +2458,7 @@ int launch_gemm_nn_gram(hipStream_t s, MvDesc A, int L, const double *M, int ldm
   case K:                                                                        \
     if (!occ[K][L]) occ[K][L] = fbg_resident(k_gemm_nn_gram<K>, lds);           \
     nb = fbg_nb(occ[K][L], nrows);                                               \
-    k_gemm_nn_gram<K><<<nb, FBG_NT, lds, s>>>(A, L, M, ldm, X, nrows, partial, pro); \
+    k_gemm_nn_gram<K><<<nb, FBG_NT, lds, s>>>(A, L, M, ldm, X, nrows, partial, pr); \
     break;
     FBG_CASES(NNG_CASE)
 #undef NNG_CASE

@@ -154,10 +154,10 @@ constexpr unsigned long long kMarch7Used =
 bool launch_spmm_march7(hipStream_t s, int n_local, const unsigned char *tid, const unsigned long long *grp, int ntpl,
                         const MarchGeom &geom, const double *vals, int nvals, MvDesc X, MvDesc Y, double alpha,
                         double beta, const double *colscale = nullptr, int sz = 0, int pd = 2, int nl = 1,
-                        const struct March27Coef *uni = nullptr);
+                        const struct March27Coef *uni = nullptr, bool all_templated = false);
 bool launch_spmm_march27(hipStream_t s, int n_local, const unsigned char *tid, const MarchGeom &geom,
                          const March27Coef &U, MvDesc X, MvDesc Y, double alpha, double beta,
-                         const double *colscale = nullptr, int sz = 0, int pd = 2);
+                         const double *colscale = nullptr, int sz = 0, int pd = 2, bool all_templated = false);
 // Templated pairs with an unused slot whose neighbour lies inside the grid (umask[t]: used slots
 // of template t, bit 6 g + i); the uniform form needs none.
 int march27_check(hipStream_t s, int npairs, const unsigned char *tid, const unsigned long long *umask, int ntpl,
@@ -170,7 +170,8 @@ int march_check(hipStream_t s, int npairs, const unsigned char *tid, const int4 
 void launch_scaled_copy(hipStream_t s, const double *a, double omega, double *out, int n);
 
 // Partial products for C = A^T B over `nrows` rows: writes nblocks x (L*kb) partials.
-int gemm_tn_blocks(int nrows);
+// workgroups (= rows of partials) of a launch over L columns (L = 0: the single-group count)
+int gemm_tn_blocks(int nrows, int L = 0);
 void launch_gemm_tn_partial(hipStream_t s, MvDesc A, int L, MvDesc B, int kb, int nrows,
                             double *partial, int nblocks);
 // out[o] = alpha * sum_b partial[b*nout + o] (fixed order: deterministic).

@@ -304,7 +304,10 @@ bool launch_spmm_sell(hipStream_t s, int n_local, const long long *off, const in
 // its three products of a block in column order, blocks in ascending order: the stored order,
 // products v * x, no FMA -- bit-identical to k_spmm_sell.  cs: fused right Jacobi scale.
 // -------------------------------------------------------------------------------------
-template <int KC, int J>
+// PF: the next group's column ids are loaded one group ahead, so a group's X segment loads
+// wait on ids that arrived during the previous group instead of on a fresh id load (the id ->
+// X dependent pair was two memory latencies per group).
+template <int KC, int J, bool PF = false>
 __global__ __launch_bounds__(256) void k_spmm_bsr3(int nbr, const long long *__restrict__ off,
                                                    const int *__restrict__ len, const int *__restrict__ bcol,
                                                    const double *__restrict__ bval, const double *__restrict__ xr,
@@ -325,14 +328,27 @@ __global__ __launch_bounds__(256) void k_spmm_bsr3(int nbr, const long long *__r
 #pragma unroll
     for (int c = 0; c < KC; ++c) s[r][c] = 0.0;
   const double *x1 = colp(X, c0);  // KC == 1: X's column directly
+  int jn[J];
+  if constexpr (PF) {
+#pragma unroll
+    for (int u = 0; u < J; ++u) jn[u] = bc[64LL * (u < L ? u : L - 1)];
+  }
   // J blocks' loads in flight together
   for (int q0 = 0; q0 < L; q0 += J) {
     int j[J];
     double v[J][9], x[J][3][KC], sc[J][3];
+    if constexpr (PF) {
+#pragma unroll
+      for (int u = 0; u < J; ++u) {
+        j[u] = jn[u];
+        const int qn = q0 + J + u < L ? q0 + J + u : L - 1;
+        jn[u] = bc[64LL * qn];
+      }
+    }
 #pragma unroll
     for (int u = 0; u < J; ++u) {
       const int q = q0 + u < L ? q0 + u : L - 1;
-      j[u] = bc[64LL * q];
+      if constexpr (!PF) j[u] = bc[64LL * q];
       // values 0..7 as four 16-byte loads of pair-interleaved strips, value 8 from its own strip
       const double *vq = bv + 9 * 64LL * q;
 #pragma unroll
@@ -399,6 +415,10 @@ void launch_spmm_bsr3(hipStream_t s, int nbr, int n_local, const long long *off,
     const char *e = std::getenv("MIGMRES_BSR3_J");
     return e ? std::atoi(e) : 2;
   }();
+  static const bool pf = [] {  // MIGMRES_BSR3_PF=1: column ids one group ahead
+    const char *e = std::getenv("MIGMRES_BSR3_PF");
+    return e && e[0] == '1';
+  }();
   const int k = Y.ncols;
   const dim3 grid(cdiv(nbr, 256)), gi(cdiv(n_local, 256));
   for (int c0 = 0; c0 < k; c0 += 8) {
@@ -408,7 +428,11 @@ void launch_spmm_bsr3(hipStream_t s, int nbr, int n_local, const long long *off,
     } else {
 #define BSR3_XR(KC)                                                                                             \
   k_interleave<KC><<<gi, 256, 0, s>>>(X, c0, kc, n_local, xr);                                                \
-  if (jsel == 4 && KC <= 4)                                                                                     \
+  if (pf && jsel == 4 && KC <= 4)                                                                               \
+    k_spmm_bsr3<KC, 4, true><<<grid, 256, 0, s>>>(nbr, off, len, bcol, bval, xr, X, Y, c0, kc, alpha, beta, cs.own); \
+  else if (pf)                                                                                                  \
+    k_spmm_bsr3<KC, 2, true><<<grid, 256, 0, s>>>(nbr, off, len, bcol, bval, xr, X, Y, c0, kc, alpha, beta, cs.own); \
+  else if (jsel == 4 && KC <= 4)                                                                                \
     k_spmm_bsr3<KC, 4><<<grid, 256, 0, s>>>(nbr, off, len, bcol, bval, xr, X, Y, c0, kc, alpha, beta, cs.own); \
   else if (jsel == 1)                                                                                           \
     k_spmm_bsr3<KC, 1><<<grid, 256, 0, s>>>(nbr, off, len, bcol, bval, xr, X, Y, c0, kc, alpha, beta, cs.own); \
@@ -1397,7 +1421,8 @@ __global__ __launch_bounds__(256) void k_spmm_march7(int npairs, int n_local, co
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
       const long long pr = (long long)q * mg.plane + soff[i];
-      r.tid[i] = (sok[i] && q >= 0 && q < mg.nz && pr < npairs) ? (int)tid[pr] : 0xFF;
+      // tid == null (uniform stencil, every pair templated): no per-pair template byte to read
+      r.tid[i] = (sok[i] && q >= 0 && q < mg.nz && pr < npairs) ? (tid ? (int)tid[pr] : 0) : 0xFF;
     }
   };
   auto operand = [&](const PlaneRegs &r, int h) __attribute__((always_inline)) {
@@ -1520,7 +1545,8 @@ __global__ __launch_bounds__(256) void k_spmm_march7(int npairs, int n_local, co
 
 bool launch_spmm_march7(hipStream_t s, int n_local, const unsigned char *tid, const unsigned long long *grp, int ntpl,
                         const MarchGeom &geom, const double *vals, int nvals, MvDesc X, MvDesc Y, double alpha,
-                        double beta, const double *colscale, int sz, int pd, int nl, const March27Coef *uni) {
+                        double beta, const double *colscale, int sz, int pd, int nl, const March27Coef *uni,
+                        bool all_templated) {
   const int npairs = (n_local + 1) / 2;
   if (npairs <= 0 || Y.ncols <= 0) return true;
   if (geom.nxp <= 0 || geom.nyl <= 0 || geom.plane != geom.nxp * geom.nyl ||
@@ -1548,6 +1574,13 @@ bool launch_spmm_march7(hipStream_t s, int n_local, const unsigned char *tid, co
       sizeof(d2) * 3 * (TY + 2) * kMarchLX + sizeof(double) * 30 * ntpl + sizeof(unsigned) * ntpl;
   const int grid = 8 * ((ntile + 7) / 8);
   const March27Coef U = uni ? *uni : March27Coef{};
+  // uniform stencil with every pair templated: the kernel needs no template id (the k-fold
+  // re-read of the N/2-byte id array, 2.6 % of the launch's bytes at k = 8)
+  static const bool keep_tid = [] {
+    const char *e = std::getenv("MIGMRES_MARCH7_TID");
+    return e && e[0] == '1';
+  }();
+  if (uni && all_templated && !keep_tid) tid = nullptr;
 #define M7U(PD, NL, UNI)                                                                                              \
   if (colscale)                                                                                                       \
     k_spmm_march7<PD, true, NL, UNI><<<grid, 256, lds, s>>>(npairs, n_local, tid, grp, ntpl, geom, txn, tyn, tzn,    \
@@ -1663,7 +1696,8 @@ __global__ __launch_bounds__(256) void k_spmm_march27(int npairs, int n_local, c
       if constexpr (CS) r.sc[h] = ok ? *(const d2 *)(cs + 2 * pc) : d2{0.0, 0.0};
     }
     const long long pr = (long long)q * mg.plane + soff[0];
-    r.tid = (sok[0] && q >= 0 && q < mg.nz && pr < npairs) ? (int)tid[pr] : 0xFF;
+    // tid == null (every pair templated): no per-pair template byte to read
+    r.tid = (sok[0] && q >= 0 && q < mg.nz && pr < npairs) ? (tid ? (int)tid[pr] : 0) : 0xFF;
   };
   auto stage = [&](const PlaneRegs &r, int q) __attribute__((always_inline)) {
     d2 *d = ring + (q & 3) * kMarchPl;
@@ -1744,7 +1778,7 @@ __global__ __launch_bounds__(256) void k_spmm_march27(int npairs, int n_local, c
 
 bool launch_spmm_march27(hipStream_t s, int n_local, const unsigned char *tid, const MarchGeom &geom,
                          const March27Coef &U, MvDesc X, MvDesc Y, double alpha, double beta, const double *colscale,
-                         int sz, int pd) {
+                         int sz, int pd, bool all_templated) {
   const int npairs = (n_local + 1) / 2;
   if (npairs <= 0 || Y.ncols <= 0) return true;
   if (geom.nxp <= 0 || geom.nyl <= 0 || geom.plane != geom.nxp * geom.nyl ||
@@ -1763,6 +1797,11 @@ bool launch_spmm_march27(hipStream_t s, int n_local, const unsigned char *tid, c
     sz = cdiv(geom.nz, slabs);
   }
   const int txn = cdiv(geom.nxp, kMarchTX), tyn = cdiv(geom.nyl, kMarchTY), tzn = cdiv(geom.nz, sz);
+  static const bool keep_tid = [] {
+    const char *e = std::getenv("MIGMRES_MARCH7_TID");
+    return e && e[0] == '1';
+  }();
+  if (all_templated && !keep_tid) tid = nullptr;
   const int grid = 8 * ((txn * tyn * tzn * Y.ncols + 7) / 8);
 #define M27T(PD, TWO)                                                                                             \
   if (colscale)                                                                                                   \
@@ -1895,7 +1934,7 @@ constexpr int TN_ROWS = 64;
 
 template <int MAXT>
 __global__ __launch_bounds__(256) void k_gemm_tn(MvDesc A, int L, MvDesc B, int kb, int nrows,
-                                                 double *__restrict__ partial) {
+                                                 double *__restrict__ partial, int contig) {
   // Branch-free main loop: every multivector keeps its padding rows [nrows, ld) at zero
   // (mv_create clears the allocation; kernels only write rows < nrows), so whole 64-row
   // chunks are read without row guards; columns past L / kb are clamped to a valid column,
@@ -1904,8 +1943,9 @@ __global__ __launch_bounds__(256) void k_gemm_tn(MvDesc A, int L, MvDesc B, int 
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int c = l & 15, g = l >> 4;
   const int ntiles = (L + 15) >> 4;
-  const int t0 = blockIdx.y * MAXT;
-  const int nt = (ntiles - t0) < MAXT ? (ntiles - t0) : MAXT;
+  const int tpg = (ntiles + gridDim.y - 1) / gridDim.y;  // tiles per group, balanced (<= MAXT)
+  const int t0 = blockIdx.y * tpg;
+  const int nt = (ntiles - t0) < tpg ? (ntiles - t0) : tpg;
   const long long nchunks = (nrows + TN_ROWS - 1) / TN_ROWS;
   const long long wid = (long long)blockIdx.x * 4 + w, nw = (long long)gridDim.x * 4;
 
@@ -1922,7 +1962,15 @@ __global__ __launch_bounds__(256) void k_gemm_tn(MvDesc A, int L, MvDesc B, int 
 #pragma unroll
   for (int tt = 0; tt < MAXT; ++tt) acc[tt] = d4{0.0, 0.0, 0.0, 0.0};
 
-  for (long long ch = wid; ch < nchunks; ch += nw) {
+  // chunk order: grid-stride (wave wid takes wid, wid + nw, ...), or (contig) workgroup b owns
+  // the contiguous range [b nchunks / G, (b + 1) nchunks / G) and its 4 waves interleave in it
+  long long cb = wid, ce = nchunks, cs = nw;
+  if (contig) {
+    cb = nchunks * blockIdx.x / gridDim.x + w;
+    ce = nchunks * (blockIdx.x + 1) / gridDim.x;
+    cs = 4;
+  }
+  for (long long ch = cb; ch < ce; ch += cs) {
     const long long r0 = ch * TN_ROWS;
     d2 bq[8], cur[8], nxt[8];
 #pragma unroll
@@ -2001,10 +2049,18 @@ static int tn_resident_blocks() {
   return cached;
 }
 
-int gemm_tn_blocks(int nrows) {
+int gemm_tn_blocks(int nrows, int L) {
   const long long waves = (nrows + TN_ROWS - 1) / TN_ROWS;
   long long b = (waves + 3) / 4;
-  const int cap = tn_resident_blocks();
+  int cap = tn_resident_blocks();
+  // MIGMRES_TN_COR=1: with several groups of column tiles (L > 16 TN_MAXT) every group's
+  // workgroups resident at once (one round) instead of group after group
+  static const bool cor = [] {
+    const char *e = std::getenv("MIGMRES_TN_COR");
+    return e && e[0] == '1';
+  }();
+  const int ny = L > 0 ? ((L + 15) / 16 + TN_MAXT - 1) / TN_MAXT : 1;
+  if (cor && ny > 1) cap = cap / ny > 0 ? cap / ny : 1;
   if (b > cap) b = cap;
   return b < 1 ? 1 : (int)b;
 }
@@ -2013,8 +2069,12 @@ void launch_gemm_tn_partial(hipStream_t s, MvDesc A, int L, MvDesc B, int kb, in
                             double *partial, int nblocks) {
   if (L > 512 || kb > 16) throw Error(MIGMRES_EINVAL, "gemm_tn: L <= 512 and kb <= 16 per launch");
   const int ntiles = (L + 15) / 16;
+  static const int contig = [] {  // MIGMRES_TN_CONTIG=1: contiguous chunk range per workgroup
+    const char *e = std::getenv("MIGMRES_TN_CONTIG");
+    return e ? std::atoi(e) : 0;
+  }();
   const dim3 grid(nblocks, (ntiles + TN_MAXT - 1) / TN_MAXT);
-  k_gemm_tn<TN_MAXT><<<grid, 256, 0, s>>>(A, L, B, kb, nrows, partial);
+  k_gemm_tn<TN_MAXT><<<grid, 256, 0, s>>>(A, L, B, kb, nrows, partial, contig);
   LAUNCH_CHECK();
 }
 

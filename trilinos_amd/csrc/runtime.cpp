@@ -582,7 +582,6 @@ void mv_trans_mv(double alpha, const migmres_mv &A, const migmres_mv &B, double 
   const int L = A.ncols, kb = B.ncols;
   if (L == 0 || kb == 0) return;
   double *red = c->red((size_t)L * kb);
-  const int nblk = gemm_tn_blocks(A.n_local);
   // Column chunks: A in 512-column slabs, B in 16-column slabs; views stay alive until the
   // stream is drained because kernels read their column tables.
   std::vector<migmres_mv *> views;
@@ -593,6 +592,7 @@ void mv_trans_mv(double alpha, const migmres_mv &A, const migmres_mv &B, double 
       views.push_back(Bv);
       for (int a0 = 0; a0 < L; a0 += 512) {
         const int lc = (L - a0) < 512 ? (L - a0) : 512;
+        const int nblk = gemm_tn_blocks(A.n_local, lc);
         migmres_mv *Av = mv_view_range(const_cast<migmres_mv *>(&A), a0, lc);
         views.push_back(Av);
         double *part = c->partial((size_t)nblk * lc * kc);
@@ -1330,11 +1330,12 @@ static void crs_apply_impl(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, d
     // templated pairs read no ghost column: they run while the halo is in flight, then the
     // pairs that do read one go to the fallback kernel
     bool done = A.use_march27 ? launch_spmm_march27(c->stream, A.n_local, A.d_tpl_id, A.march, A.march27_coef,
-                                                    X.desc(), Y.desc(), alpha, beta, cs.own, A.march_sz, A.march_pd)
+                                                    X.desc(), Y.desc(), alpha, beta, cs.own, A.march_sz, A.march_pd,
+                                                    A.n_tpl_rest == 0)
                 : A.use_march7 ? launch_spmm_march7(c->stream, A.n_local, A.d_tpl_id, A.d_tpl3_grp, A.tpl_ntpl,
                                                   A.march, A.d_tpl_val, A.tpl_nvals, X.desc(), Y.desc(), alpha,
                                                   beta, cs.own, A.march_sz, A.march_pd, A.march_nl,
-                                                  A.march_uni7 ? &A.march27_coef : nullptr)
+                                                  A.march_uni7 ? &A.march27_coef : nullptr, A.n_tpl_rest == 0)
                 : A.use_march && launch_spmm_march(c->stream, A.n_local, A.d_tpl_id, A.d_tpl3_grp, A.tpl_ntpl,
                                                    A.tpl3_G, A.march, A.d_tpl_val, A.tpl_nvals, X.desc(), Y.desc(),
                                                    alpha, beta, cs.own, A.march_kc, A.march_sz, A.march_pd);

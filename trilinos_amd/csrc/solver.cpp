@@ -329,7 +329,7 @@ struct FastIcgs {
     const char *e = std::getenv("MIGMRES_FB_GRAM_GATE");
     return e ? std::atof(e) : 0.0;
   }();
-  long long gram_calls = 0, gram_skips = 0;
+  long long gram_calls = 0, gram_skips = 0, gram_singles = 0, gram_mixed = 0;
 
   ~FastIcgs() { release(); }
   void release() {
@@ -458,12 +458,13 @@ struct FastIcgs {
         Ac.cols = A.cols + a0;
       else
         Ac.base = A.base + (long long)a0 * A.ld;
+      const int nb = gemm_tn_blocks(n_local, lc);  // <= nblk_tn (the partials buffer's rows)
       {
-        ProfScope ps(ctx, K_GEMM_TN, 8.0 * n_local * (lc + kb) + 8.0 * nblk_tn * lc * kb);
-        launch_gemm_tn_partial(ctx->stream, Ac, lc, B, kb, n_local, partial, nblk_tn);
+        ProfScope ps(ctx, K_GEMM_TN, 8.0 * n_local * (lc + kb) + 8.0 * nb * lc * kb);
+        launch_gemm_tn_partial(ctx->stream, Ac, lc, B, kb, n_local, partial, nb);
       }
-      ProfScope ps(ctx, K_REDUCE, 8.0 * nblk_tn * lc * kb);
-      launch_reduce_partials_ld(ctx->stream, partial, nblk_tn, lc, kb, ldo, 1.0, out + a0);
+      ProfScope ps(ctx, K_REDUCE, 8.0 * nb * lc * kb);
+      launch_reduce_partials_ld(ctx->stream, partial, nb, lc, kb, ldo, 1.0, out + a0);
     }
     if (ldo == L) allreduce(out, (size_t)L * kb);
   }
@@ -585,13 +586,17 @@ struct FastIcgs {
   bool gram_ok(int L, int k) const {
     // k <= 8: the closing update carries G1's partials (its LDS holds L x k coefficients);
     // 9 <= k <= 16: plain closing update, then G1 in a pass of its own (MFMA Gram kernels).
-    // DGKS (the Belos default) shares it: for k > 1 its blkOrtho is ICGS's (both passes,
-    // BelosDGKSOrthoManager.hpp:1373-1492) and its findBasis differs only in skipping the
-    // second projection of a column that kept >= dep_tol of its norm (:1094-1119), i.e. in
-    // rounding, with the same dependency test newDot < blk_tol oldDot (:1204-1210) that the
-    // Gram form takes on its pivots.  MIGMRES_FB_GRAM_DGKS=0 keeps DGKS on the column passes.
-    // A non-default "Orthogonalization Constant" keeps DGKS on the column passes.
-    return gram_on && (!slow->dgks || (gram_dgks && slow->dep_tol == 1.0 / std::sqrt(2.0))) && slow->steps == 2 && k >= 2 && L >= 1 && L <= 1024 &&
+    // DGKS (the Belos default) takes it with its own decisions: for k > 1 its blkOrtho is
+    // ICGS's (both passes, BelosDGKSOrthoManager.hpp:1373-1492), and its findBasis projects each
+    // column once and a second time only if sqrt|newDot| < dep_tol sqrt|oldDot| after the first
+    // (:1094-1119).  The first pass's newDot / oldDot of column j are the Cholesky pivot ratio
+    // R1_jj^2 / G1_jj, so k_fbg_chol takes DGKS's decision per column on it: no column asks a
+    // second projection -> CholQR1 (X T1, B = R1: one Gram-Schmidt pass per column, as DGKS);
+    // every column j >= 1 asks it -> CholQR2 (two passes, as DGKS); some do -> the column passes
+    // on the block, which decide column by column.  The dependency test newDot < blk_tol
+    // oldDot (:1204-1210) is taken on the pivots as for ICGS.  MIGMRES_FB_GRAM_DGKS=0 keeps
+    // DGKS on the column passes.
+    return gram_on && (!slow->dgks || gram_dgks) && slow->steps == 2 && k >= 2 && L >= 1 && L <= 1024 &&
            ((k <= 8 && L * k <= 7680) || (k > 8 && k <= 16));
   }
   // MIGMRES_FOLD_SMALL=0: the state reset, blk_old and C1 + C2 as separate launches
@@ -753,6 +758,8 @@ struct FastIcgs {
     }
     fetch(L, k);
     if (hst().neg != 0.0) throw Error(MIGMRES_ESTATE, "ICGS: negative definiteness in inner product");
+    if (gram && hst().gram_single) ++gram_singles;
+    if (gram && hst().gram_mixed) ++gram_mixed;
     if (gram && hst().dep == 0.0 && hst().gram_skip) {
       // a column too close to the span of the others for the Gram form: the column passes on
       // the block, which the skipped passes left holding X2
@@ -1702,7 +1709,8 @@ struct PseudoEngine : Engine {
       for (int q = 0; q < L; ++q) qcols[(size_t)(i * L + q)] = it.col(it.st[(size_t)i], q);
     MvPtr QB(mv_view(it.V.p, qcols.data(), LB));
     MvPtr X(mv_view(it.V.p, vcols.data(), n));
-    const int nblk_tn = gemm_tn_blocks(nl), nblk_nt = nn_tn_blocks(nl, LB, n), nblk_ic = icgs_blocks(nl);
+    const int nblk_tn = gemm_tn_blocks(nl), nblk_tl = gemm_tn_blocks(nl, LB), nblk_nt = nn_tn_blocks(nl, LB, n),
+              nblk_ic = icgs_blocks(nl);
     const size_t need = (size_t)4 * LB * n + 2 * (size_t)n;
     if (need > bt_cap) {
       if (bt_buf) (void)hipFree(bt_buf);
@@ -1722,11 +1730,11 @@ struct PseudoEngine : Engine {
     double *dots = M + (size_t)LB * n, *Bn = dots + n;
     {
       ProfScope ps(ctx, K_GEMM_TN, 8.0 * nl * (LB + n));
-      launch_gemm_tn_partial(s, QB->desc(), LB, X->desc(), n, nl, bt_part, nblk_tn);
+      launch_gemm_tn_partial(s, QB->desc(), LB, X->desc(), n, nl, bt_part, nblk_tl);
     }
     {
-      ProfScope ps(ctx, K_REDUCE, 8.0 * nblk_tn * LB * n);
-      launch_reduce_partials_ld(s, bt_part, nblk_tn, LB, n, LB, 1.0, C1);
+      ProfScope ps(ctx, K_REDUCE, 8.0 * nblk_tl * LB * n);
+      launch_reduce_partials_ld(s, bt_part, nblk_tl, LB, n, LB, 1.0, C1);
     }
     ctx->allreduce_async(C1, (size_t)LB * n);
     launch_blockdiag(s, C1, nullptr, LB, n, L, M1);
@@ -2261,7 +2269,7 @@ extern "C" int migmres_solver_reset(migmres_solver *s, int type) {
       s->history.clear();
       s->hist_cols = 0;
       s->n_apply = s->n_explicit = s->n_restarts = s->n_block_iters = s->n_prec = s->n_deflations = 0;
-      s->fast.gram_calls = s->fast.gram_skips = 0;
+      s->fast.gram_calls = s->fast.gram_skips = s->fast.gram_singles = s->fast.gram_mixed = 0;
     }
   });
 }
@@ -2289,7 +2297,7 @@ static int solve_impl(migmres_solver *s, migmres_crs *A, migmres_op *Aop, migmre
               "LinearProblem: inconsistent X/B/A shapes");
     s->history.clear();
     s->n_apply = s->n_explicit = s->n_restarts = s->n_block_iters = s->n_prec = s->n_deflations = 0;
-    s->fast.gram_calls = s->fast.gram_skips = 0;
+    s->fast.gram_calls = s->fast.gram_skips = s->fast.gram_singles = s->fast.gram_mixed = 0;
     s->t_spmm = s->t_ortho = s->t_lsq = s->t_check = s->t_restart = s->t_setup = 0.0;
     const double comm0 = s->ctx->comm_seconds;
     auto t0 = Clock::now();
@@ -2385,10 +2393,10 @@ extern "C" int migmres_solver_history(const migmres_solver *s, double *out, int 
 }
 extern "C" int migmres_solver_counters(const migmres_solver *s, long long *out, int n) {
   return guard([&] {
-    const long long v[9] = {s->n_apply,       s->n_explicit, s->n_restarts,        s->ortho.sing_count,
-                            s->n_block_iters, s->n_prec,     s->n_deflations,      s->fast.gram_calls,
-                            s->fast.gram_skips};
-    for (int i = 0; i < n && i < 9; ++i) out[i] = v[i];
+    const long long v[11] = {s->n_apply,       s->n_explicit, s->n_restarts,        s->ortho.sing_count,
+                             s->n_block_iters, s->n_prec,     s->n_deflations,      s->fast.gram_calls,
+                             s->fast.gram_skips, s->fast.gram_singles, s->fast.gram_mixed};
+    for (int i = 0; i < n && i < 11; ++i) out[i] = v[i];
   });
 }
 extern "C" int migmres_solver_timers(const migmres_solver *s, double *out, int n) {

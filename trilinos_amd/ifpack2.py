@@ -118,9 +118,9 @@ class Relaxation:
         return out
 
     def _free(self):
-        if self.h is not None:
+        if self.h is not None and self.A.comm.h:
             call("migmres_prec_destroy", self.h)
-            self.h = None
+        self.h = None
 
     def __del__(self):
         try:
@@ -278,9 +278,9 @@ class Chebyshev:
         return out
 
     def _free(self):
-        if self.h is not None:
+        if self.h is not None and self.A.comm.h:
             call("migmres_prec_destroy", self.h)
-            self.h = None
+        self.h = None
 
     def __del__(self):
         try:

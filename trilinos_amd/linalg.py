@@ -226,9 +226,11 @@ class CrsMatrix:
         return self.first, self.n_local
 
     def close(self):
-        if self.h:
+        # a context already destroyed (garbage cycles finalise in any order) took the operator's
+        # device memory with it: nothing left to free
+        if self.h and self.comm.h:
             call("migmres_crs_destroy", self.h)
-            self.h = None
+        self.h = None
 
     def __del__(self):
         try:
@@ -262,7 +264,7 @@ class Operator:
             self._apply(X, Y)
             return 0
         except BaseException as e:  # reported by the failing library call (MIGMRES_EOP)
-            self.error = e
+            self.error = e.with_traceback(None)  # no frame -> self reference cycle
             return 1
 
     def apply(self, X, Y):
@@ -271,9 +273,9 @@ class Operator:
     Apply = apply
 
     def close(self):
-        if self.h:
+        if self.h and self.comm.h:
             call("migmres_op_destroy", self.h)
-            self.h = None
+        self.h = None
 
     def __del__(self):
         try:
@@ -331,7 +333,7 @@ class MultiVector:
         return s.value
 
     def close(self):
-        if self.h and not self._borrowed:
+        if self.h and not self._borrowed and self.comm.h:
             call("migmres_mv_destroy", self.h)
         self.h = None
 
