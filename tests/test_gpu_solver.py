@@ -274,7 +274,7 @@ def test_dgks_orsirr1_reference_run(comm):
                 oracle_rerun(ob.solve, Aor.apply, b[:, None], dict(params, Orthogonalization="DGKS")))
 
 
-GRAM_KEYS = ("gram_calls", "gram_skips")
+GRAM_KEYS = ("gram_calls", "gram_skips", "gram_dgks_single", "gram_dgks_mixed")
 
 
 @pytest.mark.parametrize("ortho", ["ICGS", "DGKS"])
@@ -289,13 +289,16 @@ def test_gram_findbasis_against_column_passes(comm, monkeypatch, env, k, ortho):
     column passes, after the speculative SpMM has read it) and against its unfused form: the
     same solver decisions and iteration counts, histories within the oracle bar.  The Gram
     counters show which path ran (a gram_ok regression must not pass silently).
-    DGKS (the Belos default) takes the same Gram form for k > 1; against its column passes,
-    which re-orthogonalise a column only when it lost more than 1 - 1/sqrt(2) of its norm."""
+    DGKS (the Belos default) takes the Gram form for k > 1 with its own decisions (CholQR1 where
+    no column asks a second projection, the column passes where only some do); against its
+    column passes, which re-orthogonalise a column only when it lost more than 1 - 1/sqrt(2) of
+    its norm."""
     params = {"Block Size": k, "Num Blocks": 10, "Maximum Iterations": 400, "Maximum Restarts": 40,
               "Convergence Tolerance": 1e-9, "Orthogonalization": ortho}
     sm, ret, X, _, _ = _device_solve(comm, "Laplace3D", (14, 13, 12), k, 7, params)
     c = sm.counters()
-    assert c["gram_calls"] > 0 and c["gram_skips"] == 0, c
+    # DGKS hands the blocks in which only some columns ask a second projection to the column passes
+    assert c["gram_calls"] > 0 and c["gram_skips"] == c["gram_dgks_mixed"], c
     for key, v in env.items():
         monkeypatch.setenv(key, v)
     sm2, ret2, X2, _, _ = _device_solve(comm, "Laplace3D", (14, 13, 12), k, 7, params)
@@ -307,7 +310,7 @@ def test_gram_findbasis_against_column_passes(comm, monkeypatch, env, k, ortho):
     elif "MIGMRES_FB_GRAM_GATE" in env:
         assert c2["gram_skips"] == c2["gram_calls"] == c["gram_calls"]
     else:
-        assert c2["gram_calls"] == c["gram_calls"] and c2["gram_skips"] == 0
+        assert c2["gram_calls"] == c["gram_calls"] and c2["gram_skips"] == c2["gram_dgks_mixed"]
 
     def drift():
         from oracle import belos as ob, epetra as oe
@@ -374,10 +377,12 @@ def test_one_rank_rccl_transport(monkeypatch):
     assert np.array_equal(rccl[5], [1.5, -2.0])
 
 
-@pytest.mark.parametrize("kind,dims,k,nb,seed", [("Laplace3D", (16, 16, 16), 8, 6, 3),
-                                                 ("Laplace2D", (40, 25, 1), 3, 20, 2),
-                                                 ("Laplace3D", (12, 12, 12), 12, 5, 4)])
-def test_dgks_gram_decisions_match_oracle(comm, kind, dims, k, nb, seed):
+@pytest.mark.parametrize("kind,dims,k,nb,seed,drift_ok", [("Laplace3D", (16, 16, 16), 8, 6, 3, False),
+                                                          ("Laplace2D", (40, 25, 1), 3, 20, 2, False),
+                                                          # k = 12, 5 blocks per cycle: a restart every 5
+                                                          # iterations (restart-sensitive, as config 3's case)
+                                                          ("Laplace3D", (12, 12, 12), 12, 5, 4, True)])
+def test_dgks_gram_decisions_match_oracle(comm, kind, dims, k, nb, seed, drift_ok):
     """DGKS's own criterion decides in the Gram form: per block the
     device counts how many took no second projection (CholQR1), and how many had some columns
     asking it (handed to the column passes); both equal the oracle's column-by-column DGKS
@@ -398,4 +403,5 @@ def test_dgks_gram_decisions_match_oracle(comm, kind, dims, k, nb, seed):
     assert c["gram_calls"] - c["gram_skips"] - c["gram_dgks_single"] == d["fb_double"]
     record_margin("dgks_gram_decisions", dict(device=dict(single=c["gram_dgks_single"], mixed=c["gram_dgks_mixed"],
                                                           calls=c["gram_calls"], skips=c["gram_skips"]), oracle=d))
-    _hist_close(sm.residualHistory(), ref["history"], oracle_rerun(ob.solve, A.apply, A.apply(Xex), params))
+    _hist_close(sm.residualHistory(), ref["history"], oracle_rerun(ob.solve, A.apply, A.apply(Xex), params),
+                drift_ok=drift_ok)

@@ -407,6 +407,98 @@ __global__ __launch_bounds__(256) void k_spmm_bsr3(int nbr, const long long *__r
     }
 }
 
+// The same SpMM with H = 2 lanes per block row, lane h taking columns h KC/2 .. (h+1) KC/2 - 1
+// of the row-interleaved X: a block's X segment (3 rows x KC doubles, contiguous) is read by
+// the lane pair as adjacent halves, so an X load instruction touches half as many cache lines
+// per block row as the one-lane form, where every lane's 16-byte piece sat in a line of its own
+// (PMC, FlanProxy k = 4: TA 80 % and TD 91 % busy on those gathers, profiles/r4c_flan_pmc.txt).
+// Both lanes read the block's column id and 9 values (the same addresses); each output element
+// is summed in the one-lane form's order: bit-identical.
+template <int KC, int J>
+__global__ __launch_bounds__(256) void k_spmm_bsr3h(int nbr, const long long *__restrict__ off,
+                                                    const int *__restrict__ len, const int *__restrict__ bcol,
+                                                    const double *__restrict__ bval, const double *__restrict__ xr,
+                                                    MvDesc Y, int c0, int kc, double alpha, double beta,
+                                                    const double *__restrict__ cs) {
+#pragma clang fp contract(off)
+  constexpr int KH = KC / 2;  // columns per lane
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  const int b = t >> 1, h = t & 1;
+  if (b >= nbr) return;
+  const int L = len[b];
+  if (L == 0) return;  // a block row left to the row kernel
+  const long long o = off[b >> 6];
+  const int lane = b & 63;
+  const int *bc = bcol + o + lane;
+  const double *bv = bval + 9 * o + lane;
+  double s[3][KH];
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int c = 0; c < KH; ++c) s[r][c] = 0.0;
+  for (int q0 = 0; q0 < L; q0 += J) {
+    int j[J];
+    double v[J][9], x[J][3][KH], sc[J][3];
+#pragma unroll
+    for (int u = 0; u < J; ++u) {
+      const int q = q0 + u < L ? q0 + u : L - 1;
+      j[u] = bc[64LL * q];
+      const double *vq = bv + 9 * 64LL * q;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const d2 tt = *(const d2 *)(vq + 128 * m + lane);
+        v[u][2 * m] = tt.x;
+        v[u][2 * m + 1] = tt.y;
+      }
+      v[u][8] = vq[512];
+    }
+#pragma unroll
+    for (int u = 0; u < J; ++u) {
+#pragma unroll
+      for (int e = 0; e < 3; ++e) {
+        const double *xp = xr + (long long)(j[u] + e) * KC + h * KH;
+#pragma unroll
+        for (int p = 0; p < KH / 2; ++p) {
+          const d2 tt = *(const d2 *)(xp + 2 * p);
+          x[u][e][2 * p] = tt.x;
+          x[u][e][2 * p + 1] = tt.y;
+        }
+      }
+      if (cs) {
+#pragma unroll
+        for (int e = 0; e < 3; ++e) sc[u][e] = cs[j[u] + e];
+      }
+    }
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < J; ++u) {
+      if (q0 + u >= L) break;
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int e = 0; e < 3; ++e)
+#pragma unroll
+          for (int c = 0; c < KH; ++c) {
+            const double xv = cs ? sc[u][e] * x[u][e][c] : x[u][e][c];
+            s[r][c] = s[r][c] + v[u][3 * r + e] * xv;
+          }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int c = 0; c < KH; ++c) {
+      const int col = h * KH + c;
+      if (col < kc) {
+        double *yp = colp(Y, c0 + col) + 3 * b + r;
+        if (beta == 0.0)
+          *yp = (alpha == 1.0) ? s[r][c] : alpha * s[r][c];
+        else
+          *yp = alpha * s[r][c] + beta * (*yp);
+      }
+    }
+}
+
 void launch_spmm_bsr3(hipStream_t s, int nbr, int n_local, const long long *off, const int *len, const int *bcol,
                       const double *bval, MvDesc X, MvDesc Y, double alpha, double beta, double *xr,
                       ColScale cs) {
@@ -419,6 +511,10 @@ void launch_spmm_bsr3(hipStream_t s, int nbr, int n_local, const long long *off,
     const char *e = std::getenv("MIGMRES_BSR3_PF");
     return e && e[0] == '1';
   }();
+  static const int lanes = [] {  // MIGMRES_BSR3_H=2: two lanes per block row (k >= 4)
+    const char *e = std::getenv("MIGMRES_BSR3_H");
+    return e ? std::atoi(e) : 1;
+  }();
   const int k = Y.ncols;
   const dim3 grid(cdiv(nbr, 256)), gi(cdiv(n_local, 256));
   for (int c0 = 0; c0 < k; c0 += 8) {
@@ -428,7 +524,9 @@ void launch_spmm_bsr3(hipStream_t s, int nbr, int n_local, const long long *off,
     } else {
 #define BSR3_XR(KC)                                                                                             \
   k_interleave<KC><<<gi, 256, 0, s>>>(X, c0, kc, n_local, xr);                                                \
-  if (pf && jsel == 4 && KC <= 4)                                                                               \
+  if (lanes == 2 && KC >= 4)                                                                                    \
+    k_spmm_bsr3h<KC, 2><<<dim3(cdiv(2LL * nbr, 256)), 256, 0, s>>>(nbr, off, len, bcol, bval, xr, Y, c0, kc, alpha, beta, cs.own); \
+  else if (pf && jsel == 4 && KC <= 4)                                                                          \
     k_spmm_bsr3<KC, 4, true><<<grid, 256, 0, s>>>(nbr, off, len, bcol, bval, xr, X, Y, c0, kc, alpha, beta, cs.own); \
   else if (pf)                                                                                                  \
     k_spmm_bsr3<KC, 2, true><<<grid, 256, 0, s>>>(nbr, off, len, bcol, bval, xr, X, Y, c0, kc, alpha, beta, cs.own); \

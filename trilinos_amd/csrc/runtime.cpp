@@ -463,13 +463,15 @@ migmres_mv *mv_create(migmres_ctx *ctx, long long n_global, int n_local, int nco
   m->n_global = n_global;
   m->n_local = n_local;
   m->ncols = ncols;
-  // rows padded to a multiple of 64 (whole 64-row chunks, kept zero) plus 64 more rows so
+  // rows padded to a multiple of 64 (whole 64-row chunks, kept zero) plus 576 more rows so
   // that columns are not a power-of-two distance apart: with ld = 2^24 every column's row r
   // fell on the same HBM channel, and k_gemm_tn ran at 5.4 instead of 5.8-7.5 TB/s
-  // (tools/mb_lib.cpp, 256^3).
+  // (tools/mb_lib.cpp, 256^3).  576 rows (4.5 KB) from a same-box sweep of 64 .. 8256 rows at
+  // 2^21 .. 2^24 rows (the per-rank sizes of the 8/4/2/1-GPU 256^3 runs, profiles/r4d_pad*.txt):
+  // 717 -> 761, 395 -> 402, 197 -> 199, 99.4 -> 99.3 it/s against the earlier 64.
   static const long long ld_pad = [] {
     const char *e = std::getenv("MIGMRES_LD_PAD");  // rows; tuning only
-    return e ? std::atoll(e) : 64LL;
+    return e ? std::atoll(e) : 576LL;
   }();
   m->ld = round_up(n_local > 0 ? n_local : 1, 64) + ld_pad;
   m->owner = true;

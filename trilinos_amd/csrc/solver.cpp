@@ -284,6 +284,7 @@ struct FastIcgs {
   long long n_global = 0;
   int nblk_tn = 1, nblk_ic = 1;
   double *partial = nullptr, *R1 = nullptr, *R2 = nullptr, *Cout = nullptr, *red = nullptr, *S = nullptr;
+  double *cout_own = nullptr;  // Cout's own buffer (Cout may point behind the state instead)
   double *sink = nullptr;  // absorbs the padding-lane stores of the fused update kernel
   IcgsState *st = nullptr;   // current state (one of stb)
   IcgsState *stb[2] = {nullptr, nullptr};
@@ -334,7 +335,7 @@ struct FastIcgs {
   ~FastIcgs() { release(); }
   void release() {
     if (ctx) hipStreamSynchronize(ctx->stream);
-    for (void *p : {(void *)partial, (void *)R1, (void *)R2, (void *)Cout, (void *)red, (void *)S, (void *)stb[0],
+    for (void *p : {(void *)partial, (void *)R1, (void *)R2, (void *)cout_own, (void *)red, (void *)S, (void *)stb[0],
                     (void *)stb[1], (void *)sink, (void *)pbuf[1]})
       if (p) hipFree(p);
     if (ev_fetch) hipEventDestroy(ev_fetch);
@@ -343,7 +344,7 @@ struct FastIcgs {
     pbuf[0] = pbuf[1] = nullptr;
     pend = Pending{};
     if (h) hipHostFree(h);
-    partial = R1 = R2 = Cout = red = S = sink = nullptr;
+    partial = R1 = R2 = Cout = cout_own = red = S = sink = nullptr;
     st = nullptr;
     h = nullptr;
     tmpX.reset();
@@ -378,6 +379,7 @@ struct FastIcgs {
     MIG_HIP(hipMalloc(&R1, sizeof(double) * (size_t)(lmax + k) * k));
     MIG_HIP(hipMalloc(&R2, sizeof(double) * (size_t)(lmax + k) * k));
     MIG_HIP(hipMalloc(&Cout, sizeof(double) * (size_t)(lmax + k) * k));
+    cout_own = Cout;
     MIG_HIP(hipMalloc(&red, sizeof(double) * 64));
     // any nn_tn grid: at most 2048 workgroup-slots of 1024 threads' worth of lanes
     MIG_HIP(hipMalloc(&sink, sizeof(double) * 1024 * 2048));
@@ -385,8 +387,10 @@ struct FastIcgs {
     MIG_HIP(hipMalloc(&S, sbytes));
     MIG_HIP(hipMemset(S, 0, sbytes));  // zero padding row read by the row-pair kernels
     MIG_HIP(hipEventCreateWithFlags(&ev_fetch, hipEventDisableTiming));
-    MIG_HIP(hipMalloc(&stb[0], sizeof(IcgsState)));
-    MIG_HIP(hipMalloc(&stb[1], sizeof(IcgsState)));
+    // each state buffer carries a coefficient block behind it, so the block iteration's one D2H
+    // copy takes the state and the coefficients C together (fetch) when Cout sits behind st
+    for (int i = 0; i < 2; ++i)
+      MIG_HIP(hipMalloc(&stb[i], sizeof(IcgsState) + sizeof(double) * (size_t)(lmax + k) * k));
     st = stb[0];
     pbuf[0] = partial;
     MIG_HIP(hipMalloc(&pbuf[1], sizeof(double) * (size_t)nblk_ic * 17));
@@ -654,10 +658,15 @@ struct FastIcgs {
 
   void fetch(int L, int k) {
     flush_pending();
-    MIG_HIP(hipMemcpyAsync(h, st, sizeof(IcgsState), hipMemcpyDeviceToHost, ctx->stream));
-    if (L > 0)
-      MIG_HIP(hipMemcpyAsync(h + sizeof(IcgsState) / sizeof(double), Cout, sizeof(double) * (size_t)L * k,
-                             hipMemcpyDeviceToHost, ctx->stream));
+    if (L > 0 && Cout == (double *)(st + 1)) {  // one copy: the state and C behind it
+      MIG_HIP(hipMemcpyAsync(h, st, sizeof(IcgsState) + sizeof(double) * (size_t)L * k, hipMemcpyDeviceToHost,
+                             ctx->stream));
+    } else {
+      MIG_HIP(hipMemcpyAsync(h, st, sizeof(IcgsState), hipMemcpyDeviceToHost, ctx->stream));
+      if (L > 0)
+        MIG_HIP(hipMemcpyAsync(h + sizeof(IcgsState) / sizeof(double), Cout, sizeof(double) * (size_t)L * k,
+                               hipMemcpyDeviceToHost, ctx->stream));
+    }
     if (before_wait) {
       MIG_HIP(hipEventRecord(ev_fetch, ctx->stream));
       before_wait();
@@ -691,6 +700,7 @@ struct FastIcgs {
     if (k == 1 && slow->dgks) return slow->project_and_normalize(X, Q, C, ldc, B, ldb);
     ++calls;
     pend = Pending{};
+    Cout = cout_own;
     const MvDesc xd = X.desc(), qd = Q.desc();
     if (k == 1) {  // blkOrtho1, then MvDot and MvScale
       launch_state_reset(ctx->stream, st, slow->blk_tol, slow->sing_tol, slow->dgks ? 1 : 0, slow->dep_tol);
@@ -715,6 +725,8 @@ struct FastIcgs {
     // the passes reads it).
     const bool x1 = nn_then_tn(qd, L, R1, L + k, xd, k, R2);
     const bool gram = gram_ok(L, k);
+    // the Gram path takes no pending steps (st stays put): C goes behind st, one D2H copy
+    Cout = gram ? (double *)(st + 1) : cout_own;
     const bool fold = gram && gram_fuse && k <= 8 && !x1 && fold_small;
     if (!fold) {
       launch_state_reset(ctx->stream, st, slow->blk_tol, slow->sing_tol, slow->dgks ? 1 : 0, slow->dep_tol);
@@ -793,6 +805,7 @@ struct FastIcgs {
   // chain (one FastIcgs each) and waits once (fetch_async / result_k1).
   void enqueue_k1(migmres_mv &X, migmres_mv &Q) {
     const int L = Q.ncols;
+    Cout = cout_own;
     ++calls;
     pend = Pending{};
     launch_state_reset(ctx->stream, st, slow->blk_tol, slow->sing_tol, slow->dgks ? 1 : 0, slow->dep_tol);
