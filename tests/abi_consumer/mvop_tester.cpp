@@ -357,7 +357,15 @@ static bool test_operator_traits(const MV &A, const Op &M) {
   auto nc_rand_start = norms(*C, numvecs);
   for (int i = 0; i < numvecs; ++i)
     EXPECT(nc_zero_start[(size_t)i] == nc_rand_start[(size_t)i], "Apply depends on the initial destination");
-  EXPECT(!OPT::HasApplyTranspose(M), "HasApplyTranspose");
+  // A^T (migmres_crs_apply_mode): the operator is the symmetric (-1, 2, -1) tridiagonal, so A^T B
+  // equals A B up to the order of the sums
+  EXPECT(OPT::HasApplyTranspose(M), "HasApplyTranspose");
+  auto CT = MVT::Clone(*C, numvecs);
+  OPT::Apply(M, *B, *C);
+  OPT::Apply(M, *B, *CT, migmres_belos::TRANS);
+  MVT::MvAddMv(1.0, *CT, -1.0, *C, *CT);
+  auto nd = norms(*CT, numvecs), nc = norms(*C, numvecs);
+  for (int i = 0; i < numvecs; ++i) EXPECT(nd[(size_t)i] <= 1e-13 * nc[(size_t)i], "Apply(TRANS) != Apply on a symmetric operator");
   return true;
 }
 

@@ -52,6 +52,13 @@ void launch_fbg_b(hipStream_t s, MvDesc X, int k, int nrows, const IcgsState *st
 // stage 0: sums of the partials only (-> sums); 1: dependency test, R1, gate, T1; 2: R2, T2, B
 void launch_fbg_chol(hipStream_t s, const double *partial, int nblocks, int k, int stage, IcgsState *st, double *w,
                      double gate, double *sums);
+// k <= 8 with the step in the passes' prologues: sums of value-major partials (k(k+1)/2
+// values), then k_fbg_a_p (stage 1 from gsum; returns its partial rows) and k_fbg_b_p (stage 2)
+void launch_gram_sum(hipStream_t s, const double *partial, int nblocks, int k, double *sums);
+int launch_fbg_a_p(hipStream_t s, MvDesc X, int k, int nrows, IcgsState *st, double *w, const double *gsum,
+                   double gate, double *partial, int rev);
+void launch_fbg_b_p(hipStream_t s, MvDesc X, int k, int nrows, IcgsState *st, double *w, const double *gsum,
+                    double gate, int rev);
 // the same step for k > 8 from the summed Gram matrix (nv = k(k+1)/2 values)
 void launch_fbg_chol_l(hipStream_t s, const double *gsum, int k, int stage, IcgsState *st, double *w, double gate);
 

@@ -2066,6 +2066,78 @@ __global__ __launch_bounds__(FBG_NT) void k_fbg_b(MvDesc X, int nrows, const Icg
   }
 }
 
+template <int K>
+__device__ __forceinline__ void fbg_step(const double (&g)[K * (K + 1) / 2], int stage, IcgsState *st,
+                                         double *__restrict__ w, double gate, bool gw, double *Tl, int *fl);
+
+// k_fbg_a / k_fbg_b with the k x k step in their prologue (FBG_PRO): every workgroup's thread 0
+// takes the step from the all-reduced sums (the same inputs, so the same decisions on every
+// workgroup), workgroup 0 also writing the state, T and R; then the pass.  Two one-workgroup
+// launches (four with a distributed reduction) fewer per block iteration.
+template <int K>
+__global__ __launch_bounds__(FBG_NT) void k_fbg_a_p(MvDesc X, int nrows, IcgsState *st, double *__restrict__ w,
+                                                   const double *__restrict__ gsum, double gate,
+                                                   double *__restrict__ partial, int rev) {
+  constexpr int NV = K * (K + 1) / 2;
+  __shared__ double T1[16 * K];
+  __shared__ int fl[2];
+  if (threadIdx.x == 0) {
+    double g[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) g[i] = gsum[i];
+    fbg_step<K>(g, 1, st, w, gate, blockIdx.x == 0, T1, fl);
+  }
+  __syncthreads();
+  if (fl[0] || fl[1]) return;  // handed back, or DGKS's single pass (no G2)
+  double g[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) g[i] = 0.0;
+  const long long np = ((long long)nrows + 1) / 2, stride = (long long)gridDim.x * FBG_NT;
+  for (long long p = (long long)blockIdx.x * FBG_NT + threadIdx.x; p < np; p += stride) {
+    const long long r = fbg_row(p, np, rev);
+    d2 x[K];
+#pragma unroll
+    for (int c = 0; c < K; ++c) x[c] = *(const d2 *)(colp_(X, c) + r);
+    fbg_apply<K>(x, T1);
+    fbg_gram_acc<K>(x, g);
+  }
+  fbg_reduce_store<NV>(g, partial);
+}
+
+template <int K>
+__global__ __launch_bounds__(FBG_NT) void k_fbg_b_p(MvDesc X, int nrows, IcgsState *st, double *__restrict__ w,
+                                                   const double *__restrict__ gsum, double gate, int rev) {
+  constexpr int NV = K * (K + 1) / 2;
+  if (st->gram_skip) return;
+  const bool single = st->gram_single != 0;  // DGKS CholQR1: X T1 only
+  __shared__ double T1[16 * K], T2[16 * K];
+  __shared__ int fl[2];
+  for (int e = threadIdx.x; e < 16 * K; e += FBG_NT) T1[e] = w[e];
+  if (threadIdx.x == 0) {
+    fl[0] = 0;
+    if (!single) {
+      double g[NV];
+#pragma unroll
+      for (int i = 0; i < NV; ++i) g[i] = gsum[i];
+      fbg_step<K>(g, 2, st, w, gate, blockIdx.x == 0, T2, fl);
+    }
+  }
+  __syncthreads();
+  if (fl[0]) return;  // R2's gate: the block goes back to the column passes (X unchanged)
+  const long long np = ((long long)nrows + 1) / 2, stride = (long long)gridDim.x * FBG_NT;
+  for (long long p = (long long)blockIdx.x * FBG_NT + threadIdx.x; p < np; p += stride) {
+    const long long r = fbg_row(p, np, rev);
+    d2 x[K];
+#pragma unroll
+    for (int c = 0; c < K; ++c) x[c] = *(const d2 *)(colp_(X, c) + r);
+    fbg_apply<K>(x, T1);
+    if (!single) fbg_apply<K>(x, T2);
+    const bool two = r + 1 < nrows;
+#pragma unroll
+    for (int c = 0; c < K; ++c) st_pair(colp_(X, c) + r, x[c].x, x[c].y, two);
+  }
+}
+
 // findBasis in Gram form for 9 <= k <= 16.  A row pair's k(k+1)/2 register sums and the
 // hoisted T matrices no longer fit (k_fbg_b<16> spilled 708 B per lane and ran at 1.9 TB/s),
 // so both products run on v_mfma_f64_16x16x4f64:
@@ -2277,9 +2349,127 @@ __global__ __launch_bounds__(256) void k_fbg_chol_l(const double *__restrict__ g
   }
 }
 
+// The k x k step of findBasis in Gram form on the summed Gram matrix g (packed upper
+// triangle), by one thread: stage 1 = blkOrtho's dependency test on diag(G1), R1 = chol(G1)
+// with the pivot-ratio gate and DGKS's per-column decisions, T1 = R1^{-1}; stage 2 = R2, T2,
+// B = R2 R1.  gw: write the state, T and R to global memory (one workgroup does); Tl (LDS,
+// optional): T for the caller's pass; fl (optional): {hand the block back, DGKS single pass}.
+// Register arrays (fully unrolled): the factorisations are chains of dependent operations,
+// which through LDS cost tens of us.
+template <int K>
+__device__ __forceinline__ void fbg_step(const double (&g)[K * (K + 1) / 2], int stage, IcgsState *st,
+                                         double *__restrict__ w, double gate, bool gw, double *Tl, int *fl) {
+  int skip = 0, single_f = 0;
+  if (stage == 1 && gw) {
+    st->gram_skip = 0;
+    st->gram_single = 0;
+    st->gram_mixed = 0;
+    bool dep = false;
+#pragma unroll
+    for (int c = 0; c < K; ++c) dep = dep || fabs(g[c * (c + 1) / 2 + c]) < fabs(st->blk_old[c] * st->blk_tol);
+    if (dep) st->dep = 1.0;
+  }
+  // G = R^T R, R upper triangular with a positive diagonal; pivot ratios against the gate
+  double R[K][K], T[K][K];
+  bool ok = true, any2 = false, all2 = true;
+  const double dep_tol = st->dep_tol;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const double gjj = g[j * (j + 1) / 2 + j];
+    double s = gjj;
+#pragma unroll
+    for (int i = 0; i < j; ++i) s -= R[i][j] * R[i][j];
+    ok = ok && gjj > 0.0 && s >= gate * gjj;
+    if (j > 0) {  // DGKS findBasis: a second projection iff sqrt|newDot| < dep_tol sqrt|oldDot|
+      const bool two = sqrt(fabs(s)) < dep_tol * sqrt(fabs(gjj));
+      any2 = any2 || two;
+      all2 = all2 && two;
+    }
+    const double d = sqrt(fabs(s));
+    R[j][j] = d;
+#pragma unroll
+    for (int c = j + 1; c < K; ++c) {
+      double t = g[c * (c + 1) / 2 + j];
+#pragma unroll
+      for (int i = 0; i < j; ++i) t -= R[i][j] * R[i][c];
+      R[j][c] = t / d;
+    }
+  }
+  const bool dgks = stage == 1 && st->dgks;
+  if (!ok) {
+    skip = 1;
+    if (gw) st->gram_skip = 1;
+  } else if (dgks && any2 && !all2) {  // DGKS re-projects some columns only: the column passes
+    skip = 1;
+    if (gw) {
+      st->gram_skip = 1;
+      st->gram_mixed = 1;
+    }
+  } else {
+    const bool single = dgks && !any2;  // DGKS: one projection per column = CholQR1, B = R1
+    single_f = single ? 1 : 0;
+    if (single && gw) {
+      st->gram_single = 1;
+#pragma unroll
+      for (int c = 0; c < K; ++c)
+#pragma unroll
+        for (int i = 0; i <= c; ++i) st->B[i + 16 * c] = R[i][c];
+    }
+    // T = R^{-1}
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+      T[c][c] = 1.0 / R[c][c];
+#pragma unroll
+      for (int i = c - 1; i >= 0; --i) {
+        double t = 0.0;
+#pragma unroll
+        for (int m = i + 1; m <= c; ++m) t += R[i][m] * T[m][c];
+        T[i][c] = -t / R[i][i];
+      }
+    }
+    if (Tl) {
+#pragma unroll
+      for (int c = 0; c < K; ++c)
+#pragma unroll
+        for (int i = 0; i <= c; ++i) Tl[i + 16 * c] = T[i][c];
+    }
+    if (gw) {
+      double *Tout = w + (stage == 1 ? 0 : 256);
+#pragma unroll
+      for (int c = 0; c < K; ++c)
+#pragma unroll
+        for (int i = 0; i <= c; ++i) Tout[i + 16 * c] = T[i][c];
+      if (stage == 1) {
+#pragma unroll
+        for (int c = 0; c < K; ++c)
+#pragma unroll
+          for (int i = 0; i <= c; ++i) w[512 + i + 16 * c] = R[i][c];
+      } else {
+        // B = R2 R1: the reference's B (projection coefficients above the diagonal, the norms on it)
+        double R1[K][K];
+#pragma unroll
+        for (int c = 0; c < K; ++c)
+#pragma unroll
+          for (int i = 0; i <= c; ++i) R1[i][c] = w[512 + i + 16 * c];
+#pragma unroll
+        for (int c = 0; c < K; ++c)
+#pragma unroll
+          for (int i = 0; i <= c; ++i) {
+            double t = 0.0;
+#pragma unroll
+            for (int m = i; m <= c; ++m) t += R[i][m] * R1[m][c];
+            st->B[i + 16 * c] = t;
+          }
+      }
+    }
+  }
+  if (fl) {
+    fl[0] = skip;
+    fl[1] = single_f;
+  }
+}
+
 // One workgroup: the fixed-order sum of the partial rows, then thread 0 takes the step.
-// Templated on k so that G, R and T are register arrays (fully unrolled): the k x k
-// factorisations are a chain of dependent operations, which through LDS cost tens of us.
 template <int K>
 __global__ __launch_bounds__(256) void k_fbg_chol(const double *__restrict__ partial, int nblocks, int stage,
                                                   IcgsState *st, double *__restrict__ w, double gate,
@@ -2327,97 +2517,33 @@ __global__ __launch_bounds__(256) void k_fbg_chol(const double *__restrict__ par
   double g[NV];
 #pragma unroll
   for (int i = 0; i < NV; ++i) g[i] = G[i];
-  if (stage == 1) {
-    st->gram_skip = 0;
-    st->gram_single = 0;
-    st->gram_mixed = 0;
-    bool dep = false;
+  fbg_step<K>(g, stage, st, w, gate, true, nullptr, nullptr);
+}
+
+// The fixed-order sum of value-major Gram partials (partial[i * nblocks + b]): one wave per
+// value (16 waves), each lane 16 rows' loads in flight, then the wave's tree -- a few us where
+// the one-workgroup k_fbg_chol sum took ~13 us before its serial step.
+constexpr int GS_NT = 1024;
+template <int NV>
+__global__ __launch_bounds__(GS_NT) void k_gram_sum(const double *__restrict__ partial, int nblocks,
+                                                    double *__restrict__ sums) {
+  const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int i = wv; i < NV; i += GS_NT / 64) {
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int b0 = l; b0 < nblocks; b0 += 16 * 64) {
+      double x[16];
 #pragma unroll
-    for (int c = 0; c < K; ++c) dep = dep || fabs(g[c * (c + 1) / 2 + c]) < fabs(st->blk_old[c] * st->blk_tol);
-    if (dep) st->dep = 1.0;
-  }
-  // G = R^T R, R upper triangular with a positive diagonal; pivot ratios against the gate
-  double R[K][K], T[K][K];
-  bool ok = true, any2 = false, all2 = true;
-  const double dep_tol = st->dep_tol;
-#pragma unroll
-  for (int j = 0; j < K; ++j) {
-    const double gjj = g[j * (j + 1) / 2 + j];
-    double s = gjj;
-#pragma unroll
-    for (int i = 0; i < j; ++i) s -= R[i][j] * R[i][j];
-    ok = ok && gjj > 0.0 && s >= gate * gjj;
-    if (j > 0) {  // DGKS findBasis: a second projection iff sqrt|newDot| < dep_tol sqrt|oldDot|
-      const bool two = sqrt(fabs(s)) < dep_tol * sqrt(fabs(gjj));
-      any2 = any2 || two;
-      all2 = all2 && two;
-    }
-    const double d = sqrt(fabs(s));
-    R[j][j] = d;
-#pragma unroll
-    for (int c = j + 1; c < K; ++c) {
-      double t = g[c * (c + 1) / 2 + j];
-#pragma unroll
-      for (int i = 0; i < j; ++i) t -= R[i][j] * R[i][c];
-      R[j][c] = t / d;
-    }
-  }
-  if (!ok) {
-    st->gram_skip = 1;
-    return;
-  }
-  const bool dgks = stage == 1 && st->dgks;
-  if (dgks && any2 && !all2) {  // DGKS re-projects some columns only: the column passes
-    st->gram_skip = 1;
-    st->gram_mixed = 1;
-    return;
-  }
-  const bool single = dgks && !any2;  // DGKS: one projection per column = CholQR1, B = R1
-  if (single) {
-    st->gram_single = 1;
-#pragma unroll
-    for (int c = 0; c < K; ++c)
-#pragma unroll
-      for (int i = 0; i <= c; ++i) st->B[i + 16 * c] = R[i][c];
-  }
-  // T = R^{-1}
-#pragma unroll
-  for (int c = 0; c < K; ++c) {
-    T[c][c] = 1.0 / R[c][c];
-#pragma unroll
-    for (int i = c - 1; i >= 0; --i) {
-      double t = 0.0;
-#pragma unroll
-      for (int m = i + 1; m <= c; ++m) t += R[i][m] * T[m][c];
-      T[i][c] = -t / R[i][i];
-    }
-  }
-  double *Tout = w + (stage == 1 ? 0 : 256);
-#pragma unroll
-  for (int c = 0; c < K; ++c)
-#pragma unroll
-    for (int i = 0; i <= c; ++i) Tout[i + 16 * c] = T[i][c];
-  if (stage == 1) {
-#pragma unroll
-    for (int c = 0; c < K; ++c)
-#pragma unroll
-      for (int i = 0; i <= c; ++i) w[512 + i + 16 * c] = R[i][c];
-  } else {
-    // B = R2 R1: the reference's B (projection coefficients above the diagonal, the norms on it)
-    double R1[K][K];
-#pragma unroll
-    for (int c = 0; c < K; ++c)
-#pragma unroll
-      for (int i = 0; i <= c; ++i) R1[i][c] = w[512 + i + 16 * c];
-#pragma unroll
-    for (int c = 0; c < K; ++c)
-#pragma unroll
-      for (int i = 0; i <= c; ++i) {
-        double t = 0.0;
-#pragma unroll
-        for (int m = i; m <= c; ++m) t += R[i][m] * R1[m][c];
-        st->B[i + 16 * c] = t;
+      for (int u = 0; u < 16; ++u) {
+        const int b = b0 + 64 * u;
+        x[u] = b < nblocks ? partial[(long long)i * nblocks + b] : 0.0;
       }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) a[u & 3] += x[u];
+    }
+    double x = (a[0] + a[1]) + (a[2] + a[3]);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off, 64);
+    if (l == 0) sums[i] = x;
   }
 }
 
@@ -2556,6 +2682,57 @@ void launch_fbg_chol(hipStream_t s, const double *partial, int nblocks, int k, i
 #undef FC_CASE
     default:
       throw Error(MIGMRES_EINVAL, "fbg_chol: 2 <= k <= 8");
+  }
+  LAUNCH_CHECK_();
+}
+
+void launch_gram_sum(hipStream_t s, const double *partial, int nblocks, int k, double *sums) {
+  switch (k) {
+#define GSUM_CASE(K)                                                                          \
+  case K:                                                                                     \
+    k_gram_sum<K *(K + 1) / 2><<<1, GS_NT, 0, s>>>(partial, nblocks, sums);                   \
+    break;
+    FBG_CASES(GSUM_CASE)
+#undef GSUM_CASE
+    default:
+      throw Error(MIGMRES_EINVAL, "gram_sum: 2 <= k <= 8");
+  }
+  LAUNCH_CHECK_();
+}
+
+int launch_fbg_a_p(hipStream_t s, MvDesc X, int k, int nrows, IcgsState *st, double *w, const double *gsum,
+                   double gate, double *partial, int rev) {
+  static int occ[9];
+  int nb = 1;
+  switch (k) {
+#define FAP_CASE(K)                                                                    \
+  case K:                                                                              \
+    if (!occ[K]) occ[K] = fbg_resident(k_fbg_a_p<K>, 0);                               \
+    nb = fbg_nb(occ[K], nrows);                                                        \
+    k_fbg_a_p<K><<<nb, FBG_NT, 0, s>>>(X, nrows, st, w, gsum, gate, partial, rev);     \
+    break;
+    FBG_CASES(FAP_CASE)
+#undef FAP_CASE
+    default:
+      throw Error(MIGMRES_EINVAL, "fbg_a_p: 2 <= k <= 8");
+  }
+  LAUNCH_CHECK_();
+  return nb;
+}
+
+void launch_fbg_b_p(hipStream_t s, MvDesc X, int k, int nrows, IcgsState *st, double *w, const double *gsum,
+                    double gate, int rev) {
+  static int occ[9];
+  switch (k) {
+#define FBP_CASE(K)                                                                                  \
+  case K:                                                                                            \
+    if (!occ[K]) occ[K] = fbg_resident(k_fbg_b_p<K>, 0);                                             \
+    k_fbg_b_p<K><<<fbg_nb(occ[K], nrows), FBG_NT, 0, s>>>(X, nrows, st, w, gsum, gate, rev);         \
+    break;
+    FBG_CASES(FBP_CASE)
+#undef FBP_CASE
+    default:
+      throw Error(MIGMRES_EINVAL, "fbg_b_p: 2 <= k <= 8");
   }
   LAUNCH_CHECK_();
 }

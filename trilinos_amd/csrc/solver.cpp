@@ -603,6 +603,11 @@ struct FastIcgs {
     return gram_on && (!slow->dgks || gram_dgks) && slow->steps == 2 && k >= 2 && L >= 1 && L <= 1024 &&
            ((k <= 8 && L * k <= 7680) || (k > 8 && k <= 16));
   }
+  // MIGMRES_FBG_PRO=0: k <= 8 takes the k x k steps in one-workgroup launches (k_fbg_chol)
+  bool fbg_pro = [] {
+    const char *e = std::getenv("MIGMRES_FBG_PRO");
+    return !(e && e[0] == '0');
+  }();
   // MIGMRES_FOLD_SMALL=0: the state reset, blk_old and C1 + C2 as separate launches
   bool fold_small = [] {
     const char *e = std::getenv("MIGMRES_FOLD_SMALL");
@@ -615,7 +620,7 @@ struct FastIcgs {
   void gram_alloc() {
     if (gb.part) return;
     MIG_HIP(hipMalloc(&gb.part, sizeof(double) * 1024 * 136));
-    MIG_HIP(hipMalloc(&gb.sum, sizeof(double) * 136));
+    MIG_HIP(hipMalloc(&gb.sum, sizeof(double) * 272));
     MIG_HIP(hipMalloc(&gb.w, sizeof(double) * 768));
   }
   // findBasis in Gram form (icgs.hip): CholQR2 of the block with the reference's dependency
@@ -641,6 +646,32 @@ struct FastIcgs {
       }
     };
     const int rev = nb1 ? 1 : 0;  // sweep directions alternate from pass to pass
+    if (k <= 8 && fbg_pro) {
+      // the k x k steps in the passes' prologues: sum (+ all-reduce) -> pass -> sum -> pass
+      if (!nb1) {
+        ProfScope ps(ctx, K_FB, 8.0 * n * k);
+        nb1 = launch_fbg_gram(ctx->stream, X, k, n_local, gb.part, 1);
+      }
+      double *s1 = gb.sum, *s2 = gb.sum + 136;
+      {
+        ProfScope ps(ctx, K_REDUCE, 8.0 * nb1 * nv);
+        launch_gram_sum(ctx->stream, gb.part, nb1, k, s1);
+        allreduce(s1, (size_t)nv);
+      }
+      int nb2;
+      {
+        ProfScope ps(ctx, K_FB, 8.0 * n * k);
+        nb2 = launch_fbg_a_p(ctx->stream, X, k, n_local, st, gb.w, s1, gate, gb.part, rev);
+      }
+      {
+        ProfScope ps(ctx, K_REDUCE, 8.0 * nb2 * nv);
+        launch_gram_sum(ctx->stream, gb.part, nb2, k, s2);
+        allreduce(s2, (size_t)nv);
+      }
+      ProfScope ps(ctx, K_FB, 16.0 * n * k);
+      launch_fbg_b_p(ctx->stream, X, k, n_local, st, gb.w, s2, gate, 1 - rev);
+      return;
+    }
     if (!nb1) {
       ProfScope ps(ctx, K_FB, 8.0 * n * k);
       nb1 = launch_fbg_gram(ctx->stream, X, k, n_local, gb.part, 1);
