@@ -1326,7 +1326,10 @@ static void crs_apply_impl(migmres_crs &A, const migmres_mv &X, migmres_mv &Y, d
     MIG_HIP(hipEventRecord(c->ev_halo, c->halo_stream));
     c->comm_seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
-  ProfScope ps(c, K_SPMM, A.spmm_fixed_bytes + 8.0 * A.n_local * k * (beta == 0.0 ? 2.0 : 3.0) +
+  // the uniform march kernels with every pair templated read no template id: X and Y only
+  const bool no_ids = A.use_tpl && A.use_march && (A.march_uni7 || A.use_march27) && A.n_tpl_rest == 0 &&
+                      !env_on("MIGMRES_MARCH7_TID");
+  ProfScope ps(c, K_SPMM, (no_ids ? 0.0 : A.spmm_fixed_bytes) + 8.0 * A.n_local * k * (beta == 0.0 ? 2.0 : 3.0) +
                             (cs.own ? 8.0 * A.n_local : 0.0));
   if (A.use_tpl) {
     // templated pairs read no ghost column: they run while the halo is in flight, then the
