@@ -560,7 +560,9 @@ void launch_spmm_bsr3(hipStream_t s, int nbr, int n_local, const long long *off,
 // -------------------------------------------------------------------------------------
 constexpr int PAIR_MAXR = 8;
 
-template <int KC, int PAIR_MAXK>
+// CS: the fused right Jacobi's column scale (a template flag, so the plain form holds no scale
+// registers: 154 -> fewer VGPRs, one more wave per SIMD)
+template <int KC, int PAIR_MAXK, bool CS>
 __global__ __launch_bounds__(256) void k_spmm_pair(int npairs, int rmax, const double *__restrict__ sv,
                                                    const int *__restrict__ sk,
                                                    const unsigned short *__restrict__ sm, MvDesc X, int n_local,
@@ -615,8 +617,8 @@ __global__ __launch_bounds__(256) void k_spmm_pair(int npairs, int rmax, const d
   }
   // fused right Jacobi: per key the (omega d^-1) pair of its two columns (the owner's values
   // for ghost columns, imported once); zero padding past the last row / ghost
-  d2 sc[PAIR_MAXK];
-  if (cs) {
+  d2 sc[CS ? PAIR_MAXK : 1];
+  if constexpr (CS) {
 #pragma unroll
     for (int u = 0; u < PAIR_MAXK; ++u)
       sc[u] = *(const d2 *)(key[u] >= 0 ? cs + 2LL * key[u] : gcs + 2LL * (-key[u] - 1));
@@ -632,7 +634,7 @@ __global__ __launch_bounds__(256) void k_spmm_pair(int npairs, int rmax, const d
       const int kk = key[u];
       const double *src = kk >= 0 ? xc + 2LL * kk : gc + 2LL * (-kk - 1);
       d2 x = *(const d2 *)src;
-      if (cs) x = sc[u] * x;
+      if constexpr (CS) x = sc[u] * x;
       const double pa0 = cx[u][0] * x.x, pa1 = cx[u][1] * x.y;
       const double pb0 = cx[u][2] * x.x, pb1 = cx[u][3] * x.y;
       sa = sa + ((use >> (4 * u)) & 1ull ? pa0 : 0.0);
@@ -667,14 +669,23 @@ static void spmm_pair_cols(hipStream_t s, int npairs, int rmax, const double *sv
   const dim3 grid(cdiv(units, 256));
   for (int c0 = 0; c0 < k; c0 += 8) {
     const int kc = (k - c0) < 8 ? (k - c0) : 8;
-    if (kc == 1)
-      k_spmm_pair<1, MAXK><<<grid, 256, 0, s>>>(npairs, rmax, sv, sk, sm, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel, cs.own, cs.ghost);
-    else if (kc <= 2)
-      k_spmm_pair<2, MAXK><<<grid, 256, 0, s>>>(npairs, rmax, sv, sk, sm, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel, cs.own, cs.ghost);
-    else if (kc <= 4)
-      k_spmm_pair<4, MAXK><<<grid, 256, 0, s>>>(npairs, rmax, sv, sk, sm, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel, cs.own, cs.ghost);
-    else
-      k_spmm_pair<8, MAXK><<<grid, 256, 0, s>>>(npairs, rmax, sv, sk, sm, X, n_local, ghost, ldg, Y, c0, kc, alpha, beta, sel, nsel, cs.own, cs.ghost);
+#define PAIR_KC(KC)                                                                                              \
+  if (cs.own)                                                                                                    \
+    k_spmm_pair<KC, MAXK, true><<<grid, 256, 0, s>>>(npairs, rmax, sv, sk, sm, X, n_local, ghost, ldg, Y, c0, kc,  \
+                                                     alpha, beta, sel, nsel, cs.own, cs.ghost);                  \
+  else                                                                                                           \
+    k_spmm_pair<KC, MAXK, false><<<grid, 256, 0, s>>>(npairs, rmax, sv, sk, sm, X, n_local, ghost, ldg, Y, c0, kc, \
+                                                      alpha, beta, sel, nsel, nullptr, nullptr);
+    if (kc == 1) {
+      PAIR_KC(1)
+    } else if (kc <= 2) {
+      PAIR_KC(2)
+    } else if (kc <= 4) {
+      PAIR_KC(4)
+    } else {
+      PAIR_KC(8)
+    }
+#undef PAIR_KC
     LAUNCH_CHECK();
   }
 }
