@@ -142,18 +142,7 @@ void launch_spmm(hipStream_t s, int row_begin, int row_end, const int *rowptr, c
 // XR: the owned operands come from xr, a row-interleaved copy of X's columns c0 .. c0 + KC - 1
 // (k_interleave): one entry's KC values are KC / 2 16-byte loads of one 8 KC-byte segment
 // (one cache line) instead of KC 8-byte gathers from KC lines.  Same values, same order.
-// xr slot of owned row r: r, or 4 (r / 3) + r % 3 in the node-padded layout (launch_spmm_bsr3)
-template <bool PAD3>
-__device__ __forceinline__ long long xr_slot(int r) {
-  if constexpr (PAD3) {
-    const int q = r / 3;
-    return 4LL * q + (r - 3 * q);
-  } else {
-    return r;
-  }
-}
-
-template <int KC, bool XR = false, bool PAD3 = false>
+template <int KC, bool XR = false>
 __global__ __launch_bounds__(256) void k_spmm_sell(int n, const long long *__restrict__ off,
                                                    const int *__restrict__ len, const int *__restrict__ scol,
                                                    const double *__restrict__ sval, MvDesc X, int n_local,
@@ -210,7 +199,7 @@ __global__ __launch_bounds__(256) void k_spmm_sell(int n, const long long *__res
         sc[j] = cs ? (own ? cs[col] : gcs[col - n_local]) : 1.0;
         if constexpr (XR) {
           if (own) {
-            const d2 *xp = (const d2 *)(xr + xr_slot<PAD3>(col) * KC);
+            const d2 *xp = (const d2 *)(xr + (long long)col * KC);
 #pragma unroll
             for (int h = 0; h < KC / 2; ++h) {
               const d2 q = xp[h];
@@ -251,23 +240,22 @@ __global__ __launch_bounds__(256) void k_spmm_sell(int n, const long long *__res
   }
 }
 
-// xr[slot(r)][c] = X[r][c0 + c] for c < kc, 0 beyond (KC-wide rows; the node-padded layout's
-// fourth row of a node is never read)
-template <int KC, bool PAD3 = false>
+// xr[r][c] = X[r][c0 + c] for c < kc, 0 beyond (KC-wide rows)
+template <int KC>
 __global__ __launch_bounds__(256) void k_interleave(MvDesc X, int c0, int kc, int n, double *__restrict__ xr) {
   const int r = blockIdx.x * 256 + threadIdx.x;
   if (r >= n) return;
   double v[KC];
 #pragma unroll
   for (int c = 0; c < KC; ++c) v[c] = c < kc ? colp(X, c0 + c)[r] : 0.0;
-  d2 *out = (d2 *)(xr + xr_slot<PAD3>(r) * KC);
+  d2 *out = (d2 *)(xr + (long long)r * KC);
 #pragma unroll
   for (int h = 0; h < KC / 2; ++h) out[h] = d2{v[2 * h], v[2 * h + 1]};
 }
 
 bool launch_spmm_sell(hipStream_t s, int n_local, const long long *off, const int *len, const int *scol,
                       const double *sval, MvDesc X, const double *ghost, long long ldg, MvDesc Y, double alpha,
-                      double beta, const int *sel, int nsel, double *xr, bool xr_ready, ColScale cs, bool pad3) {
+                      double beta, const int *sel, int nsel, double *xr, bool xr_ready, ColScale cs) {
   const int n = sel ? nsel : n_local;
   if (n <= 0) return xr_ready;  // nothing launched: xr is as it was
   const int k = Y.ncols;
@@ -279,16 +267,10 @@ bool launch_spmm_sell(hipStream_t s, int n_local, const long long *off, const in
       // xr_ready: an earlier launch of the same apply (interior rows) already interleaved X;
       // only with one column chunk, since xr holds one chunk at a time
       const bool fresh = !(xr_ready && k <= 8);
-#define SELL_XR_P(KC, P)                                                                                            \
-  if (fresh) k_interleave<KC, P><<<gi, 256, 0, s>>>(X, c0, kc, n_local, xr);                                      \
-  k_spmm_sell<KC, true, P><<<grid, 256, 0, s>>>(n_local, off, len, scol, sval, X, n_local, ghost, ldg, Y, c0, kc, \
-                                                alpha, beta, sel, nsel, xr, cs.own, cs.ghost);
-#define SELL_XR(KC)      \
-  if (pad3) {            \
-    SELL_XR_P(KC, true)  \
-  } else {               \
-    SELL_XR_P(KC, false) \
-  }
+#define SELL_XR(KC)                                                                                            \
+  if (fresh) k_interleave<KC><<<gi, 256, 0, s>>>(X, c0, kc, n_local, xr);                                    \
+  k_spmm_sell<KC, true><<<grid, 256, 0, s>>>(n_local, off, len, scol, sval, X, n_local, ghost, ldg, Y, c0, kc, \
+                                             alpha, beta, sel, nsel, xr, cs.own, cs.ghost);
       if (kc <= 2) {
         SELL_XR(2)
       } else if (kc <= 4) {
@@ -297,7 +279,6 @@ bool launch_spmm_sell(hipStream_t s, int n_local, const long long *off, const in
         SELL_XR(8)
       }
 #undef SELL_XR
-#undef SELL_XR_P
       LAUNCH_CHECK();
       xr_ready = k <= 8;  // xr holds this (only) chunk now
       continue;
@@ -384,7 +365,7 @@ __global__ __launch_bounds__(256) void k_spmm_bsr3(int nbr, const long long *__r
 #pragma unroll
         for (int e = 0; e < 3; ++e) x[u][e][0] = x1[j[u] + e];
       } else {
-        const d2 *xp = (const d2 *)(xr + xr_slot<true>(j[u]) * KC);  // j[u] = 3 node: slot 4 node
+        const d2 *xp = (const d2 *)(xr + (long long)j[u] * KC);
 #pragma unroll
         for (int h = 0; h < 3 * KC / 2; ++h) {
           const d2 t = xp[h];
@@ -475,7 +456,7 @@ __global__ __launch_bounds__(256) void k_spmm_bsr3h(int nbr, const long long *__
     for (int u = 0; u < J; ++u) {
 #pragma unroll
       for (int e = 0; e < 3; ++e) {
-        const double *xp = xr + (xr_slot<true>(j[u]) + e) * KC + h * KH;
+        const double *xp = xr + (long long)(j[u] + e) * KC + h * KH;
 #pragma unroll
         for (int p = 0; p < KH / 2; ++p) {
           const d2 tt = *(const d2 *)(xp + 2 * p);
@@ -542,7 +523,7 @@ void launch_spmm_bsr3(hipStream_t s, int nbr, int n_local, const long long *off,
       k_spmm_bsr3<1, 4><<<grid, 256, 0, s>>>(nbr, off, len, bcol, bval, nullptr, X, Y, c0, kc, alpha, beta, cs.own);
     } else {
 #define BSR3_XR(KC)                                                                                             \
-  k_interleave<KC, true><<<gi, 256, 0, s>>>(X, c0, kc, n_local, xr);                                          \
+  k_interleave<KC><<<gi, 256, 0, s>>>(X, c0, kc, n_local, xr);                                                \
   if (lanes == 2 && KC >= 4)                                                                                    \
     k_spmm_bsr3h<KC, 2><<<dim3(cdiv(2LL * nbr, 256)), 256, 0, s>>>(nbr, off, len, bcol, bval, xr, Y, c0, kc, alpha, beta, cs.own); \
   else if (pf && jsel == 4 && KC <= 4)                                                                          \
@@ -1692,9 +1673,9 @@ bool launch_spmm_march7(hipStream_t s, int n_local, const unsigned char *tid, co
     }
     // slabs: about MIGMRES_MARCH_WPC (default 2) work items per CU over all (column, tile) work
     // items, at least 8 planes per slab (each slab re-reads 2 halo planes).  With 8-line tiles,
-    // same box (profiles/r4_knob_sweeps.txt, sweep_r4m_*): the 8-GPU per-rank shapes run their
-    // SpMM x 8 in 0.047 ms (256 x 256 x 32: one slab) and 0.049 ms (128^3: 32-plane slabs)
-    // against 0.054 ms with the earlier ~9 items per CU (7- and 8-plane slabs).
+    // same box (profiles/r4_knob_sweeps.txt, sweep_r4m_* / sweep_r4n_*): 256^3 SpMM x 8 0.449 ->
+    // 0.420 ms (one 256-plane slab instead of five), and the 8-GPU per-rank shapes 0.054 ->
+    // 0.047 ms (256 x 256 x 32: one slab) and 0.049 ms (128^3: 32-plane slabs).
     static const int wpc = [] {
       const char *e = std::getenv("MIGMRES_MARCH_WPC");
       const int v = e ? std::atoi(e) : 2;
@@ -1929,7 +1910,12 @@ bool launch_spmm_march27(hipStream_t s, int n_local, const unsigned char *tid, c
         cus = 256;
     }
     const long long cols = (long long)cdiv(geom.nxp, kMarchTX) * cdiv(geom.nyl, kMarchTY) * Y.ncols;
-    const long long slabs = std::max(1LL, std::min((long long)cdiv(9LL * cus, cols), (long long)cdiv(geom.nz, 4)));
+    static const int wpc = [] {  // work items per CU (MIGMRES_MARCH27_WPC), as launch_spmm_march7's
+      const char *e = std::getenv("MIGMRES_MARCH27_WPC");
+      const int v = e ? std::atoi(e) : 9;
+      return v > 0 ? v : 9;
+    }();
+    const long long slabs = std::max(1LL, std::min((long long)cdiv((long long)wpc * cus, cols), (long long)cdiv(geom.nz, 4)));
     sz = cdiv(geom.nz, slabs);
   }
   const int txn = cdiv(geom.nxp, kMarchTX), tyn = cdiv(geom.nyl, kMarchTY), tzn = cdiv(geom.nz, sz);
