@@ -93,15 +93,19 @@ def test_config_solves_match_oracle(comm, case):
            drift_ok=case in RESTART_SENSITIVE)
 
 
-@pytest.mark.parametrize("dims,nb,P", [((20, 20, 20), 24, 1), ((18, 17, 16), 23, 2)])
-def test_k16_full_cycle_matches_oracle(comm, dims, nb, P):
+@pytest.mark.parametrize("dims,nb,P,m16", [((20, 20, 20), 24, 1, "1"), ((18, 17, 16), 23, 2, "1"),
+                                            ((20, 20, 20), 24, 1, "0")])
+def test_k16_full_cycle_matches_oracle(comm, monkeypatch, dims, nb, P, m16):
     """Config 3's block size through a whole long cycle (tol 1e-15: never converges, so every
     block step runs): L = 16 .. 16 (nb - 1), which takes the fused update + projection through
-    each of its k = 16 forms in the default selection (MIGMRES_NW16=1) -- 32-row chunks (L = 64
+    each of its k = 16 forms -- by default (MIGMRES_NT_M16=1) the 16x16x4 form k_nn_tn_m16 from
+    L = 48 on (two workgroups per CU up to L = 256, one beyond) and the per-wave-rows form
+    below; with MIGMRES_NT_M16=0 the earlier selection (MIGMRES_NW16=1): 32-row chunks (L = 64
     .. 128 and 272 .. 336), 16-row chunks in two 256-thread workgroups per CU (L = 160 .. 256;
     C1 in registers up to L = 208) and 512-thread 16-row workgroups (L = 352, 368) -- and the
     Gram-form findBasis at k = 16; counts and residual history against the oracle."""
     import trilinos_amd as ta
+    monkeypatch.setenv("MIGMRES_NT_M16", m16)
     k = 16
     params = _params(k, nb, **{"Convergence Tolerance": 1e-15, "Maximum Iterations": nb, "Maximum Restarts": 0})
     n, gen = _gen("Laplace3D", dims)

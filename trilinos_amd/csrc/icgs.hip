@@ -1016,7 +1016,209 @@ __global__ __launch_bounds__(256) void k_nn_tn_pw(MvDesc Q, int L, const double 
   (void)sink;
 }
 
+// -------------------------------------------------------------------------------------
+// k > 8 (<= 16): the fused update + projection with both products on v_mfma_f64_16x16x4f64 and
+// C1 in registers (round 4).  The 4x4x4 forms above hold C1's B operand 4-fold replicated (the
+// same 4 x 4 block for each of the four row blocks of an instruction), so a 32-row image with
+// C1 in registers did not fit and C1 went to LDS (L x 16 doubles), which kept the 32-row image
+// (256-byte column visits) at one workgroup per CU from L ~ 144 on.  Here phase 1 forms the
+// TRANSPOSED update, D1^T = C1^T Qc^T: the A operand C1^T[j][4 s + kk] = C1[4 s + (l >> 4)][l & 15]
+// is one register per lane and K step (L / 16 per wave with the K dimension split in quarters),
+// the B operand Qc^T[4 s + kk][row] is the staged image's column-major element, and lane l ends
+// with D1 for chunk row 16 rb + (l & 15), X columns (l >> 4) + 4 r.  Phase 2 accumulates
+// C2 += Qc^T X1 per 16-column tile of Q (A = image, B = X1 from the image's X columns).
+// 512 threads = 2 row blocks x 4 K quarters; the quarters are summed in a fixed order,
+// ((q0 + q2) + (q1 + q3)), through an 8 KB buffer, so the LDS is the image + 8 KB: two
+// workgroups per CU up to L = 256 at k = 16.  Read-only (X1 stays in the LDS image).
+// -------------------------------------------------------------------------------------
+static size_t m16_lds_bytes(int L) {
+  const size_t lp = (size_t)((L + 16 + 15) & ~15);
+  return sizeof(double) * (lp * 33 + 4 * 256);
+}
+
+template <int LQ, int WPE>
+__global__ __launch_bounds__(512, WPE) void k_nn_tn_m16(MvDesc Q, int L, const double *__restrict__ C1, int ldc,
+                                                        MvDesc X, int k, int nrows, double *__restrict__ partial,
+                                                        double *__restrict__ sink) {
+  // LQ = ceil(L / 16): MS = LQ K steps per wave in phase 1 (4 LQ steps of 4 over the quarters),
+  // TPW 16-column tiles per wave in phase 2, NM 32-column loads per lane for the L + 16 image
+  // columns.  Steps and tiles past L read image columns >= L (X or zero columns, all inside the
+  // image) against zero C1 entries / into discarded rows, so they add exact zeros.  Q and X
+  // are plain (no column table).
+  constexpr int RW = 32, LDQ = RW + 1, LPC = RW / 2, CPR = 512 / LPC;
+  constexpr int MS = LQ, TPW = (LQ + 7) / 8, NM = (LQ + 2) / 2;
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const int Lp = (L + 16 + 15) & ~15, LX = L + k;
+  double *Qs = sm;
+  double *red = sm + (size_t)Lp * LDQ;
+  const int t = threadIdx.x, l = t & 63, c = l & 15, g = l >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int rb = w & 1, kq = w >> 1;
+  for (int e = t; e < Lp * LDQ + 4 * 256; e += 512) sm[e] = 0.0;
+  // phase 1's A operands for the K steps s = kq + 4 m of this wave
+  double c1r[MS];
+#pragma unroll
+  for (int m = 0; m < MS; ++m) {
+    const int i = 4 * (kq + 4 * m) + g;
+    c1r[m] = (i < L && c < k) ? C1[i + (long long)c * ldc] : 0.0;
+  }
+  d4 acc[TPW];
+#pragma unroll
+  for (int mm = 0; mm < TPW; ++mm) acc[mm] = d4{0.0, 0.0, 0.0, 0.0};
+  // loader: image column lcol + 32 m (clamped to LX - 1), rows lrow, lrow + 1 of the chunk
+  const int lrow = 2 * (t % LPC), lcol = t / LPC;
+  // (image column of load m: one register each; the 64-bit source address and the LDS slot are
+  // re-derived per chunk, which keeps the wide images out of scratch)
+  int lci[NM];
+#pragma unroll
+  for (int m = 0; m < NM; ++m) {
+    const int i = lcol + CPR * m;
+    lci[m] = i < LX ? i : LX - 1;
+  }
+  auto lsrc = [&](int m, long long r0) __attribute__((always_inline)) {
+    const int i = lci[m];
+    return (const d2 *)((i < L ? Q.base + (long long)i * Q.ld : X.base + (long long)(i - L) * X.ld) + lrow + r0);
+  };
+  const long long nchunks = (nrows + RW - 1) / RW;
+  const long long c0 = nchunks * blockIdx.x / gridDim.x, c1 = nchunks * (blockIdx.x + 1) / gridDim.x;
+  d2 p[NM];
+  if (c0 < c1) {
+#pragma unroll
+    for (int m = 0; m < NM; ++m) p[m] = *lsrc(m, c0 * RW);
+  }
+  lds_barrier();  // the zeroed image
+  const double *b1 = Qs + g * LDQ + 16 * rb + c + 4 * kq * LDQ;  // phase 1, step m: + 16 m LDQ
+  for (long long ch = c0; ch < c1; ++ch) {
+#pragma unroll
+    for (int m = 0; m < NM; ++m) {
+      const int o = lci[m] * LDQ + lrow;
+      Qs[o] = p[m].x;
+      Qs[o + 1] = p[m].y;
+    }
+    lds_barrier();
+    {
+      const long long nx = (ch + 1 < c1 ? ch + 1 : ch) * RW;
+#pragma unroll
+      for (int m = 0; m < NM; ++m) p[m] = *lsrc(m, nx);
+    }
+    // phase 1: D1^T (16 X columns x 16 chunk rows of row block rb), K quarter kq, in batches of
+    // 4 K steps (a batch's LDS reads, then its MFMAs: the empty asm statements keep the
+    // compiler from hoisting every read of the chunk)
+    d4 d = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int m0 = 0; m0 < MS; m0 += 4) {
+      double b[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (m0 + u < MS) b[u] = b1[16 * (m0 + u) * LDQ];
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (m0 + u < MS) d = __builtin_amdgcn_mfma_f64_16x16x4f64(c1r[m0 + u], b[u], d, 0, 0, 0);
+      asm volatile("" : "+v"(d)::"memory");  // the batch's MFMAs stay ahead of the next batch's reads
+    }
+    // fixed-order sum of the K quarters: (q0 + q2) + (q1 + q3)
+    if (kq >= 2) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[((kq - 2) * 2 + rb) * 256 + 64 * r + l] = d[r];
+    }
+    lds_barrier();
+    if (kq < 2) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) d[r] = d[r] + red[(kq * 2 + rb) * 256 + 64 * r + l];
+    }
+    if (kq == 1) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[(2 + rb) * 256 + 64 * r + l] = d[r];
+    }
+    lds_barrier();
+    if (kq == 0) {
+      // X1 = X - D1 into the image's X columns (columns >= k: zero minus zero)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        double *xs = Qs + (size_t)(L + g + 4 * r) * LDQ + 16 * rb + c;
+        *xs = *xs - (d[r] + red[(2 + rb) * 256 + 64 * r + l]);
+      }
+    }
+    lds_barrier();
+    // phase 2: C2 tile (16 Q columns x 16 X columns) += Qc^T X1, tiles w, w + 8, ... (< L / 16:
+    // a wave-uniform bound)
+#pragma unroll
+    for (int sp = 0; sp < RW / 4; ++sp) {
+      const double xb = Qs[(L + c) * LDQ + 4 * sp + g];
+      double a[TPW];
+#pragma unroll
+      for (int mm = 0; mm < TPW; ++mm)
+        if (16 * (w + 8 * mm) < L) a[mm] = Qs[(16 * (w + 8 * mm) + c) * LDQ + 4 * sp + g];
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int mm = 0; mm < TPW; ++mm) {
+        if (16 * (w + 8 * mm) < L) acc[mm] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mm], xb, acc[mm], 0, 0, 0);
+        asm volatile("" : "+v"(acc[mm])::"memory");
+      }
+    }
+    lds_barrier();
+  }
+  // partial (L x k, column-major) of this workgroup: D[Q column 16 tt + g + 4 r][X column c]
+  double *out = partial + (long long)blockIdx.x * L * k;
+#pragma unroll
+  for (int mm = 0; mm < TPW; ++mm) {
+    const int tt = w + 8 * mm;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = 16 * tt + g + 4 * r;
+      if (16 * tt < L && i < L && c < k) out[i + (long long)c * L] = acc[mm][r];
+    }
+  }
+  (void)sink;
+}
+
 typedef void (*nt_kernel_t)(MvDesc, int, const double *, int, MvDesc, int, int, double *, double *);
+
+// The 16x16x4 form (k_nn_tn_m16): MIGMRES_NT_M16 = 0 off, 1 (default) from L = M16_MIN_L on,
+// 2 every k > 8 shape from L = 16 (read per launch, so a test can switch it).
+constexpr int M16_MIN_L = 48;
+static int m16_mode() {
+  const char *e = std::getenv("MIGMRES_NT_M16");
+  return e ? std::atoi(e) : 1;
+}
+static bool m16_ok(int L, int k) {
+  const int m = m16_mode();
+  return m != 0 && k > 8 && k <= 16 && L >= (m >= 2 ? 16 : M16_MIN_L) && L + 16 <= 512;
+}
+// One instantiation per 16-column step of L; two workgroups per CU (4 waves per SIMD: 128
+// registers) up to L = 240, else one.  Measured (tools/mb_k16.cpp, 256^3, k = 16, same box,
+// profiles/r4q_k16_nn_tn_sweep.txt) against the forms above: L = 64 2.42 -> 2.16 ms, 128 4.56 ->
+// 3.62, 208 6.63 -> 5.66 (5.3 TB/s), 272 9.86 -> 8.00, 400 13.35 -> 11.56; L = 256 with two
+// workgroups per CU spilled (24 registers) and ran at 4.36 TB/s, hence one there.  Below L = 48
+// the per-wave-rows form stays ahead (L = 16: 0.86 vs 1.19 ms).
+static nt_kernel_t m16_pick(int L) {
+  switch ((L + 15) >> 4) {
+#define M16_CASE(N) \
+  case N:           \
+    return k_nn_tn_m16<N, (N <= 15 ? 4 : 2)>;
+    M16_CASE(1) M16_CASE(2) M16_CASE(3) M16_CASE(4) M16_CASE(5) M16_CASE(6) M16_CASE(7) M16_CASE(8)
+    M16_CASE(9) M16_CASE(10) M16_CASE(11) M16_CASE(12) M16_CASE(13) M16_CASE(14) M16_CASE(15) M16_CASE(16)
+    M16_CASE(17) M16_CASE(18) M16_CASE(19) M16_CASE(20) M16_CASE(21) M16_CASE(22) M16_CASE(23) M16_CASE(24)
+    M16_CASE(25) M16_CASE(26) M16_CASE(27) M16_CASE(28) M16_CASE(29) M16_CASE(30) M16_CASE(31)
+#undef M16_CASE
+    default: return nullptr;
+  }
+}
+// resident workgroups per CU (LDS and registers), cached per image width
+static int m16_per_cu(int L) {
+  static int cache[513] = {};
+  int &v = cache[L];
+  if (!v) {
+    int per_cu = 0;
+    const nt_kernel_t f = m16_pick(L);
+    if (hipFuncSetAttribute((const void *)f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, 512, m16_lds_bytes(L)) != hipSuccess)
+      per_cu = 1;
+    v = per_cu < 1 ? 1 : per_cu > 2 ? 2 : per_cu;
+  }
+  return v;
+}
 
 static int pw_mode() {
   static int m = -1;
@@ -1194,7 +1396,7 @@ static bool nw_ok(int L, int k) {
   if (k > 8) return k <= 16 && (nw_single16(L, k) || nw_ok(L, 8));  // all columns, or halves in one launch
   return L >= 64 && L + k <= 512 && nw_wg_per_cu(L, k) >= 1;
 }
-bool nn_tn_paired(int L, int k) { return k > 8 && !pw_ok(L, k) && !nw_single16(L, k); }
+bool nn_tn_paired(int L, int k) { return k > 8 && !m16_ok(L, k) && !pw_ok(L, k) && !nw_single16(L, k); }
 
 static int cu_count() {
   static int cus = 0;
@@ -1208,6 +1410,12 @@ static int cu_count() {
 }
 
 int nn_tn_blocks(int nrows, int L, int k) {
+  if (m16_ok(L, k)) {
+    const long long nchunks = (nrows + 31) / 32;
+    long long b = (long long)m16_per_cu(L) * cu_count();
+    if (b > nchunks) b = nchunks;
+    return b < 1 ? 1 : (int)b;
+  }
   if (pw_ok(L, k)) {
     const long long nchunks = (nrows + 15) / 16;
     long long b = (long long)pw_per_cu(L) * cu_count();
@@ -1240,7 +1448,7 @@ int nn_tn_blocks(int nrows, int L, int k) {
 }
 
 bool nn_tn_supported(int L, int k) {
-  return L >= 1 && k >= 1 && k <= 16 && (L <= NT_MAXL || nw_ok(L, k) || pw_ok(L, k));
+  return L >= 1 && k >= 1 && k <= 16 && (L <= NT_MAXL || m16_ok(L, k) || nw_ok(L, k) || pw_ok(L, k));
 }
 
 void launch_nn_tn(hipStream_t s, MvDesc Q, int L, const double *C1, int ldc, MvDesc X, int nrows,
@@ -1248,6 +1456,14 @@ void launch_nn_tn(hipStream_t s, MvDesc Q, int L, const double *C1, int ldc, MvD
   const int k = X.ncols;
   if (!nn_tn_supported(L, k))
     throw Error(MIGMRES_EINVAL, "nn_tn: 1 <= k <= 16 and L <= 256 (L + k <= 512 for k <= 8, L >= 64)");
+  if (m16_ok(L, k) && !Q.cols && !X.cols) {
+    if (store_x1) throw Error(MIGMRES_EINVAL, "nn_tn: k > 8 is read-only");
+    m16_per_cu(L);  // raises the kernel's dynamic LDS limit
+    hipLaunchKernelGGL(m16_pick(L), dim3(nblocks), dim3(512), m16_lds_bytes(L), s, Q, L, C1, ldc, X, k, nrows,
+                       partial, sink);
+    LAUNCH_CHECK_();
+    return;
+  }
   if (pw_ok(L, k)) {
     if (store_x1) throw Error(MIGMRES_EINVAL, "nn_tn: k > 8 is read-only");
     const int LT = 16 * ((L + 15) >> 4);

@@ -1910,12 +1910,9 @@ bool launch_spmm_march27(hipStream_t s, int n_local, const unsigned char *tid, c
         cus = 256;
     }
     const long long cols = (long long)cdiv(geom.nxp, kMarchTX) * cdiv(geom.nyl, kMarchTY) * Y.ncols;
-    static const int wpc = [] {  // work items per CU (MIGMRES_MARCH27_WPC), as launch_spmm_march7's
-      const char *e = std::getenv("MIGMRES_MARCH27_WPC");
-      const int v = e ? std::atoi(e) : 9;
-      return v > 0 ? v : 9;
-    }();
-    const long long slabs = std::max(1LL, std::min((long long)cdiv((long long)wpc * cus, cols), (long long)cdiv(geom.nz, 4)));
+    // (about 9 work items per CU; 2 or 4, which helped the 7-point march, measured equal here:
+    // Brick3D + Jacobi 256^3 fused SpMM 0.574-0.581 ms either way, sweep_r4p_bj)
+    const long long slabs = std::max(1LL, std::min((long long)cdiv(9LL * cus, cols), (long long)cdiv(geom.nz, 4)));
     sz = cdiv(geom.nz, slabs);
   }
   const int txn = cdiv(geom.nxp, kMarchTX), tyn = cdiv(geom.nyl, kMarchTY), tzn = cdiv(geom.nz, sz);
