@@ -1,7 +1,12 @@
-set -o pipefail
-B="timeout -k 10 300 python bench.py --steps 50 --warmup 10 --no-cpu-baseline"
-$B > gpurun_out/sec_headline.json 2> gpurun_out/sec_headline.err && \
-$B --solver GMRES > gpurun_out/sec_pseudo.json 2> gpurun_out/sec_pseudo.err && \
-$B --prec right > gpurun_out/sec_jacobi.json 2> gpurun_out/sec_jacobi.err && \
-$B --solver "FLEXIBLE GMRES" --prec right --sweeps 2 > gpurun_out/sec_flex.json 2> gpurun_out/sec_flex.err && \
-$B --matrix Brick3D --prec right > gpurun_out/sec_brick.json 2> gpurun_out/sec_brick.err
+# Secondary bench lines of a round (one per DESIGN section 7 row): PROF names the outputs.
+source ./tools/gpu/step.sh
+P=${PROF:-sec}
+B="python bench.py --no-cpu-baseline"
+step 300 bench_k16_$P.json $B --k 16 --no-csr-spmm
+step 300 bench_bj_$P.json $B --matrix Brick3D --prec right --no-csr-spmm
+step 300 bench_flan_$P.json $B --matrix FlanProxy --k 4
+step 300 bench_dgks_$P.json $B --ortho DGKS --no-csr-spmm
+step 300 bench_pseudo_$P.json $B --solver GMRES --no-csr-spmm
+step 300 bench_cheb_$P.json $B --matrix Brick3D --prec right --prec-type chebyshev --no-csr-spmm
+MIGMRES_FORCE_RCCL=1 step 300 bench_nz32_$P.json $B --nz 32 --no-csr-spmm
+for f in k16 bj flan dgks pseudo cheb nz32; do python3 tools/bench_summary.py gpurun_out/bench_${f}_$P.json $f; done
