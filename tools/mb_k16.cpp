@@ -63,7 +63,7 @@ int main(int argc, char **argv) {
   hipStream_t s = 0;
   const int nblk = gemm_tn_blocks((int)n);
   for (int k : {8, 16}) {
-    for (int L : {16, 32, 48, 64, 96, 128, 144, 160, 192, 208, 224, 256, 272, 320, 336, 352, 400}) {
+    for (int L : {8, 16, 24, 32, 40, 48, 56, 64, 96, 128, 144, 160, 192, 208, 224, 256, 272, 320, 336, 352, 400}) {
       if (L + k > Lmax) continue;
       MvDesc A{V, ld, nullptr, L + k};
       MvDesc X{V + (long long)L * ld, ld, nullptr, k};

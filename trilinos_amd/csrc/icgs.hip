@@ -1184,6 +1184,7 @@ static int m16_mode() {
 }
 static bool m16_ok(int L, int k) {
   const int m = m16_mode();
+  if (m == 3 && k >= 2 && k <= 8 && L >= 16 && L < 64) return true;  // k <= 8 below the wide kernels
   return m != 0 && k > 8 && k <= 16 && L >= (m >= 2 ? 16 : M16_MIN_L) && L + 16 <= 512;
 }
 // One instantiation per 16-column step of L; two workgroups per CU (4 waves per SIMD: 128
