@@ -1314,8 +1314,8 @@ static nt_kernel_t nw_pick_nm(int LX) {
 }
 
 
-// The wide variant wins from L = 64 on (256^3, k = 8); below that the per-chunk latency
-// is not hidden.  Up to L + k = 256 NW_WG_PER_CU workgroups' LDS fit in 160 KiB; wider
+// The wide variant wins from L = 16 on at k = 8 (round 4, see nw_min_l; it used to win only from
+// L = 64, where the per-chunk latency was not hidden below).  Up to L + k = 256 NW_WG_PER_CU workgroups' LDS fit in 160 KiB; wider
 // images (k = 16 in column halves: L up to 400 at Num Blocks 25) run one workgroup per CU.
 // k > 8 with all columns in one workgroup can also run on 16-row chunks (256 threads): the
 // image takes half the LDS, so two workgroups share a CU up to L = 256 and one barrier-bound
@@ -1393,9 +1393,18 @@ static int nw_wg_per_cu(int L, int k) {
 // workgroup pairs on one XCD (paired: every chunk of Q enters two CUs, from HBM once and from
 // L2 / the Infinity Cache once -- twice the bytes into the CUs, which is what bounds it).
 static bool nw_single16(int L, int k) { return k > 8 && k <= 16 && L >= 64 && L + k <= 512 && nw_wg_per_cu(L, k) >= 1; }
+// Smallest L of the wide form at k <= 8 (MIGMRES_NW_MIN_L, read per call): 16 for 4 <= k <= 8,
+// where it now beats the narrow k_nn_tn at every L (256^3 k = 8, tools/mb_k16.cpp,
+// profiles/r4u_k8_small_l.txt: L = 16 1.15 -> 0.94 ms, 48 1.97 -> 1.45, 56 2.10 -> 1.58; same-box
+// bench lines, sweep_r4v_*: 256^3 99.1 -> 100.0 it/s, FlanProxy k = 4 1285 -> 1306), 64 below
+// k = 4 (not measured).
+static int nw_min_l(int k) {
+  const char *e = std::getenv("MIGMRES_NW_MIN_L");
+  return e ? std::atoi(e) : (k >= 4 ? 16 : 64);
+}
 static bool nw_ok(int L, int k) {
-  if (k > 8) return k <= 16 && (nw_single16(L, k) || nw_ok(L, 8));  // all columns, or halves in one launch
-  return L >= 64 && L + k <= 512 && nw_wg_per_cu(L, k) >= 1;
+  if (k > 8) return k <= 16 && (nw_single16(L, k) || (L >= 64 && nw_ok(L, 8)));  // all columns, or halves
+  return L >= nw_min_l(k) && L + k <= 512 && nw_wg_per_cu(L, k) >= 1;
 }
 bool nn_tn_paired(int L, int k) { return k > 8 && !m16_ok(L, k) && !pw_ok(L, k) && !nw_single16(L, k); }
 

@@ -499,6 +499,120 @@ __global__ __launch_bounds__(256) void k_spmm_bsr3h(int nbr, const long long *__
     }
 }
 
+// Cooperative form (the default, launch_spmm_bsr3): the X segments of a wave's 64 J blocks are loaded by
+// consecutive lanes as consecutive 16-byte pieces (a segment's 3 KC / 2 pieces by neighbouring
+// lanes, so a load instruction covers ~64 / (3 KC / 2) whole segments instead of one piece of
+// 64 scattered ones), staged in a wave-private LDS slice, and read back by their owners.  The
+// column ids go through LDS the same way.  Every lane of the wave takes part in the loads until
+// the wave's longest block row is done; lanes past their own row length (or past nbr) add
+// nothing and store nothing.  Same products and order as k_spmm_bsr3: bit-identical.
+template <int KC, int J>
+__global__ __launch_bounds__(256) void k_spmm_bsr3c(int nbr, const long long *__restrict__ off,
+                                                    const int *__restrict__ len, const int *__restrict__ bcol,
+                                                    const double *__restrict__ bval, const double *__restrict__ xr,
+                                                    MvDesc Y, int c0, int kc, double alpha, double beta,
+                                                    const double *__restrict__ cs) {
+#pragma clang fp contract(off)
+  constexpr int S2 = 3 * KC / 2, NI = J * S2;
+  __shared__ __attribute__((aligned(16))) d2 seg[4][64 * NI];
+  __shared__ int jl[4][64 * J];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  const bool live = b < nbr;
+  const int L = live ? len[b] : 0;
+  int Lw = L;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) Lw = max(Lw, __shfl_xor(Lw, o, 64));
+  if (Lw == 0) return;  // the whole wave: nothing to do
+  const long long o = live ? off[b >> 6] : 0;
+  const int *bc = bcol + o + lane;
+  const double *bv = bval + 9 * o + lane;
+  d2 *sg = seg[w];
+  int *jw = jl[w];
+  double s[3][KC];
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int c = 0; c < KC; ++c) s[r][c] = 0.0;
+  for (int q0 = 0; q0 < Lw; q0 += J) {
+    int j[J];
+    double v[J][9], x[J][3][KC], sc[J][3];
+#pragma unroll
+    for (int u = 0; u < J; ++u) {
+      const bool on = q0 + u < L;
+      const int q = on ? q0 + u : 0;
+      j[u] = on ? bc[64LL * q] : 0;
+      if (on) {
+        const double *vq = bv + 9 * 64LL * q;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const d2 t = *(const d2 *)(vq + 128 * m + lane);
+          v[u][2 * m] = t.x;
+          v[u][2 * m + 1] = t.y;
+        }
+        v[u][8] = vq[512];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 9; ++e) v[u][e] = 0.0;
+      }
+      jw[u * 64 + lane] = j[u];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    d2 pc[NI];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int p = i * 64 + lane, sidx = p / S2, m = p - sidx * S2;
+      pc[i] = *(const d2 *)(xr + (long long)jw[sidx] * KC + 2 * m);
+    }
+#pragma unroll
+    for (int i = 0; i < NI; ++i) sg[i * 64 + lane] = pc[i];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int u = 0; u < J; ++u) {
+#pragma unroll
+      for (int h = 0; h < S2; ++h) {
+        const d2 t = sg[(u * 64 + lane) * S2 + h];
+        x[u][(2 * h) / KC][(2 * h) % KC] = t.x;
+        x[u][(2 * h + 1) / KC][(2 * h + 1) % KC] = t.y;
+      }
+      if (cs) {
+#pragma unroll
+        for (int e = 0; e < 3; ++e) sc[u][e] = cs[j[u] + e];
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();  // the slice is rewritten by the next step
+#pragma unroll
+    for (int u = 0; u < J; ++u) {
+      if (q0 + u >= L) break;
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int e = 0; e < 3; ++e)
+#pragma unroll
+          for (int c = 0; c < KC; ++c) {
+            const double xv = cs ? sc[u][e] * x[u][e][c] : x[u][e][c];
+            s[r][c] = s[r][c] + v[u][3 * r + e] * xv;
+          }
+    }
+  }
+  if (L == 0) return;  // a block row left to the row kernel (or past nbr)
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+      if (c < kc) {
+        double *yp = colp(Y, c0 + c) + 3 * b + r;
+        if (beta == 0.0)
+          *yp = (alpha == 1.0) ? s[r][c] : alpha * s[r][c];
+        else
+          *yp = alpha * s[r][c] + beta * (*yp);
+      }
+    }
+}
+
 void launch_spmm_bsr3(hipStream_t s, int nbr, int n_local, const long long *off, const int *len, const int *bcol,
                       const double *bval, MvDesc X, MvDesc Y, double alpha, double beta, double *xr,
                       ColScale cs) {
@@ -515,6 +629,13 @@ void launch_spmm_bsr3(hipStream_t s, int nbr, int n_local, const long long *off,
     const char *e = std::getenv("MIGMRES_BSR3_H");
     return e ? std::atoi(e) : 1;
   }();
+  // Cooperative segment loads (k_spmm_bsr3c, default; MIGMRES_BSR3_C=0: k_spmm_bsr3).  Same box,
+  // FlanProxy (profiles/r4_knob_sweeps.txt, sweep_r4t_*): k = 4 SpMM 0.300 -> 0.281 ms and
+  // 0.291 -> 0.272 ms (two blocks per lane and step; one: equal), k = 8 0.440 -> 0.387 ms.
+  static const bool coop = [] {
+    const char *e = std::getenv("MIGMRES_BSR3_C");
+    return !(e && e[0] == '0');
+  }();
   const int k = Y.ncols;
   const dim3 grid(cdiv(nbr, 256)), gi(cdiv(n_local, 256));
   for (int c0 = 0; c0 < k; c0 += 8) {
@@ -524,7 +645,13 @@ void launch_spmm_bsr3(hipStream_t s, int nbr, int n_local, const long long *off,
     } else {
 #define BSR3_XR(KC)                                                                                             \
   k_interleave<KC><<<gi, 256, 0, s>>>(X, c0, kc, n_local, xr);                                                \
-  if (lanes == 2 && KC >= 4)                                                                                    \
+  if (coop && jsel == 1)                                                                                        \
+    k_spmm_bsr3c<KC, 1><<<grid, 256, 0, s>>>(nbr, off, len, bcol, bval, xr, Y, c0, kc, alpha, beta, cs.own);    \
+  else if (coop && KC <= 4)                                                                                     \
+    k_spmm_bsr3c<KC, 2><<<grid, 256, 0, s>>>(nbr, off, len, bcol, bval, xr, Y, c0, kc, alpha, beta, cs.own);    \
+  else if (coop)                                                                                                \
+    k_spmm_bsr3c<KC, 1><<<grid, 256, 0, s>>>(nbr, off, len, bcol, bval, xr, Y, c0, kc, alpha, beta, cs.own);    \
+  else if (lanes == 2 && KC >= 4)                                                                               \
     k_spmm_bsr3h<KC, 2><<<dim3(cdiv(2LL * nbr, 256)), 256, 0, s>>>(nbr, off, len, bcol, bval, xr, Y, c0, kc, alpha, beta, cs.own); \
   else if (pf && jsel == 4 && KC <= 4)                                                                          \
     k_spmm_bsr3<KC, 4, true><<<grid, 256, 0, s>>>(nbr, off, len, bcol, bval, xr, X, Y, c0, kc, alpha, beta, cs.own); \
