@@ -2972,17 +2972,18 @@ void launch_fbg_chol_l(hipStream_t s, const double *gsum, int k, int stage, Icgs
 
 // -------------------------------------------------------------------------------------
 // Batched k = 1 ICGS for pseudo-block GMRES (solver.cpp, PseudoEngine::batched_ortho): the n
-// right-hand sides' bases side by side as one column table QB (n blocks of L columns) and
+// right-hand sides' bases interleaved as QB (column q n + i = basis vector q of right-hand side
+// i: a plain contiguous range of the iteration-major basis while every slot is active) and
 // their new vectors as X (n columns).  The block kernels form every cross product QB^T X;
-// right-hand side j keeps its own block (rows j L .. j L + L - 1 of column j), the rest is
-// masked to zero, so each column is projected against its own basis only.
+// right-hand side j keeps its own entries (rows q n + j of column j), the rest is masked to
+// zero, so each column is projected against its own basis only.
 // -------------------------------------------------------------------------------------
 __global__ void k_blockdiag(const double *__restrict__ C1, const double *__restrict__ C2, int LB, int n, int L,
                             double *__restrict__ M) {
   const int e = blockIdx.x * 256 + threadIdx.x;
   if (e >= LB * n) return;
   const int r = e % LB, j = e / LB;
-  const bool mine = r / L == j;
+  const bool mine = r % n == j;  // QB's column r = q n + i belongs to right-hand side i
   M[e] = mine ? (C2 ? C1[e] + C2[e] : C1[e]) : 0.0;
 }
 void launch_blockdiag(hipStream_t s, const double *C1, const double *C2, int LB, int n, int L, double *M) {

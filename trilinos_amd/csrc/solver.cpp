@@ -1689,9 +1689,12 @@ struct Engine {
 // ------------------------------------------------------------------------------------
 // Pseudo-block GMRES: k single-vector GMRES iterations sharing one operator application per
 // step (BelosPseudoBlockGmresIter.hpp, BelosPseudoBlockGmresSolMgr.hpp).  Right-hand side i
-// owns the basis slot V[:, slot*(nb+1) .. slot*(nb+1)+nb] of one device multivector; its
-// Hessenberg column, Givens rotations and least-squares right-hand side stay on the host.
-// Deflation of converged right-hand sides drops their state; slots are never moved.
+// owns the basis columns V[:, j*nslots + slot], j = 0 .. nb, of one device multivector
+// (iteration-major, so while every slot is active the bases of step c are the contiguous
+// columns 0 .. (c+1) nslots - 1, and the new vectors the next nslots: the batched ICGS reads
+// them without a column table); its Hessenberg column, Givens rotations and least-squares
+// right-hand side stay on the host.  Deflation of converged right-hand sides drops their
+// state; slots are never moved.
 // ------------------------------------------------------------------------------------
 struct PseudoRhs {
   int slot;
@@ -1699,10 +1702,16 @@ struct PseudoRhs {
 };
 
 struct PseudoIter {
-  int nb = 0, cur_dim = 0, num_iters = 0;
+  int nb = 0, cur_dim = 0, num_iters = 0, nslots = 0;
   MvPtr V;  // N x nslots*(nb+1)
   std::vector<PseudoRhs> st;
-  int col(const PseudoRhs &r, int j) const { return r.slot * (nb + 1) + j; }
+  int col(const PseudoRhs &r, int j) const { return j * nslots + r.slot; }
+  // basis columns first .. first + cnt - 1 of one right-hand side (a column-table view)
+  MvPtr basis(const PseudoRhs &r, int first, int cnt) const {
+    std::vector<int> idx((size_t)cnt);
+    for (int q = 0; q < cnt; ++q) idx[(size_t)q] = col(r, first + q);
+    return MvPtr(mv_view(V.p, idx.data(), cnt));
+  }
   double &Hat(PseudoRhs &r, int i, int j) const { return r.H[(size_t)i + (size_t)j * (nb + 1)]; }
 };
 
@@ -1749,8 +1758,8 @@ struct PseudoEngine : Engine {
     hipStream_t s = ctx->stream;
     const int n = (int)it.st.size(), L = c + 1, LB = n * L, nl = lp.X->n_local;
     std::vector<int> qcols((size_t)LB);
-    for (int i = 0; i < n; ++i)
-      for (int q = 0; q < L; ++q) qcols[(size_t)(i * L + q)] = it.col(it.st[(size_t)i], q);
+    for (int q = 0; q < L; ++q)  // iteration-major: contiguous while every slot is active
+      for (int i = 0; i < n; ++i) qcols[(size_t)(q * n + i)] = it.col(it.st[(size_t)i], q);
     MvPtr QB(mv_view(it.V.p, qcols.data(), LB));
     MvPtr X(mv_view(it.V.p, vcols.data(), n));
     const int nblk_tn = gemm_tn_blocks(nl), nblk_tl = gemm_tn_blocks(nl, LB), nblk_nt = nn_tn_blocks(nl, LB, n),
@@ -1807,7 +1816,7 @@ struct PseudoEngine : Engine {
     const double *Mh = bt_host, *Bh = bt_host + (size_t)LB * n + n;
     for (int i = 0; i < n; ++i) {
       PseudoRhs &rs = it.st[(size_t)i];
-      for (int q = 0; q <= c; ++q) it.Hat(rs, q, c) = Mh[(size_t)(i * L + q) + (size_t)i * LB];
+      for (int q = 0; q <= c; ++q) it.Hat(rs, q, c) = Mh[(size_t)(q * n + i) + (size_t)i * LB];
       it.Hat(rs, c + 1, c) = Bh[i];
     }
   }
@@ -1838,7 +1847,7 @@ struct PseudoEngine : Engine {
         for (int u = q + 1; u < c; ++u) t -= it.Hat(r, q, u) * y[(size_t)u];
         y[(size_t)q] = t / it.Hat(r, q, q);
       }
-      MvPtr Vi = view(*it.V, it.col(r, 0), c);
+      MvPtr Vi = it.basis(r, 0, c);
       MvPtr ui = view(*upd, i, 1);
       mv_times_mat_add_mv(1.0, *Vi, y.data(), c, 0.0, *ui);
     }
@@ -1899,7 +1908,7 @@ struct PseudoEngine : Engine {
         for (int i = 0; i < n; ++i) {
           PseudoRhs &rs = it.st[(size_t)i];
           ws.push_back(view(*it.V, vcols[(size_t)i], 1));
-          qs.push_back(view(*it.V, it.col(rs, 0), c + 1));
+          qs.push_back(it.basis(rs, 0, c + 1));
           FastIcgs &f = rhs_ortho(rs.slot);
           f.enqueue_k1(*ws.back(), *qs.back());
           f.fetch_async(c + 1, 1);
@@ -1917,7 +1926,7 @@ struct PseudoEngine : Engine {
         for (int i = 0; i < n; ++i) {
           PseudoRhs &rs = it.st[(size_t)i];
           MvPtr w = view(*it.V, vcols[(size_t)i], 1);
-          MvPtr Q = view(*it.V, it.col(rs, 0), c + 1);
+          MvPtr Q = it.basis(rs, 0, c + 1);
           S->ortho.project_and_normalize(*w, *Q, h.data(), c + 1, r.data(), 1);
           for (int q = 0; q <= c; ++q) it.Hat(rs, q, c) = h[(size_t)q];
           it.Hat(rs, c + 1, c) = r[0];
@@ -1984,6 +1993,7 @@ struct PseudoEngine : Engine {
     S->ortho.dep_tol = p.dgks_dep_tol();
     PseudoIter it;
     it.nb = p.num_blocks;
+    it.nslots = block;
     it.V = MvPtr(mv_create(lp.X->ctx, lp.X->n_global, lp.X->n_local, block * (p.num_blocks + 1)));
     rhs_nb = p.num_blocks;
     rhs_fast.clear();
