@@ -377,6 +377,57 @@ def test_one_rank_rccl_transport(monkeypatch):
     assert np.array_equal(rccl[5], [1.5, -2.0])
 
 
+@pytest.mark.parametrize("gram_dgks", ["1", "0"])
+def test_dgks_second_projection_fires(comm, monkeypatch, gram_dgks):
+    """DGKS parity where its conditional second projection actually fires: A =
+    diag(1 + i/n) + 100 u u^T, whose dominant rank-one part leaves a new block's columns nearly
+    parallel after blkOrtho, so the oracle's column-by-column DGKS findBasis
+    (BelosDGKSOrthoManager.hpp:1094-1119) re-projects every column of some blocks and some
+    columns of another.  The device -- in the Gram form (CholQR1 / CholQR2 / column passes per
+    block, MIGMRES_FB_GRAM_DGKS=1) and with DGKS's column passes (=0) -- takes the same number of
+    iterations and restarts, the Gram form the same decision counts, and the history follows the
+    oracle within the drift bar: the case is rounding-sensitive by construction -- the oracle
+    re-run with reversed inner-product sums moves its own history by 9.8e-11 -- and both device
+    forms sit at that size (1.0e-10 Gram form, 8.4e-11 column passes, MI355X).  Same host-built
+    B for both."""
+    import trilinos_amd as ta
+    from oracle import belos as ob, epetra as oe
+    monkeypatch.setenv("MIGMRES_FB_GRAM_DGKS", gram_dgks)
+    n, k = 300, 4
+    rng = np.random.default_rng(1)
+    u = rng.standard_normal(n)
+    u /= np.linalg.norm(u)
+    Ad = np.diag(1.0 + np.arange(n) / n) + 100.0 * np.outer(u, u)
+    Aor = oe.DistCrs(lambda f, m: (np.arange(m + 1) * n, np.tile(np.arange(n), m), Ad[f:f + m].ravel()), n, 1)
+    Xex, _ = oe.epetra_random_mv(5, n, k)
+    B = Aor.apply(Xex)
+    params = {"Num Blocks": 10, "Block Size": k, "Maximum Iterations": 400, "Maximum Restarts": 30,
+              "Convergence Tolerance": 1e-10, "Orthogonalization": "DGKS"}
+    ref = ob.solve(Aor.apply, B, params)
+    d = ref["fb_decisions"]
+    assert d["fb_double"] >= 1 and d["fb_mixed"] >= 1  # the case does exercise the second projection
+    first, nloc = ta.uniform_map(n, comm.nranks, comm.rank)
+    A = ta.CrsMatrix(comm, n, np.arange(nloc + 1) * n, np.tile(np.arange(n), nloc), Ad[first:first + nloc].ravel())
+    X, Bd = ta.MultiVector(comm, n, k), ta.MultiVector(comm, n, k)
+    X.put_scalar(0.0)
+    Bd.upload(B)
+    lp = ta.LinearProblem(A, X, Bd)
+    assert lp.setProblem()
+    sm = ta.BlockGmresSolMgr(lp, params)
+    sm.solve()
+    c = sm.counters()
+    assert sm.getNumIters() == ref["iterations"]
+    assert c["restarts"] == ref["restarts"]
+    if gram_dgks == "1":
+        assert c["gram_dgks_single"] == d["fb_single"]
+        assert c["gram_dgks_mixed"] == d["fb_mixed"]
+        assert c["gram_calls"] - c["gram_skips"] - c["gram_dgks_single"] == d["fb_double"]
+    record_margin("dgks_gram_decisions", dict(device=dict(single=c["gram_dgks_single"], mixed=c["gram_dgks_mixed"],
+                                                          calls=c["gram_calls"], skips=c["gram_skips"]),
+                                              oracle=d, gram_dgks=gram_dgks))
+    _hist_close(sm.residualHistory(), ref["history"], oracle_rerun(ob.solve, Aor.apply, B, params), drift_ok=True)
+
+
 @pytest.mark.parametrize("kind,dims,k,nb,seed,drift_ok", [("Laplace3D", (16, 16, 16), 8, 6, 3, False),
                                                           ("Laplace2D", (40, 25, 1), 3, 20, 2, False),
                                                           # k = 12, 5 blocks per cycle: a restart every 5
