@@ -1176,7 +1176,8 @@ __global__ __launch_bounds__(512, WPE) void k_nn_tn_m16(MvDesc Q, int L, const d
 typedef void (*nt_kernel_t)(MvDesc, int, const double *, int, MvDesc, int, int, double *, double *);
 
 // The 16x16x4 form (k_nn_tn_m16): MIGMRES_NT_M16 = 0 off, 1 (default) from L = M16_MIN_L on,
-// 2 every k > 8 shape from L = 16 (read per launch, so a test can switch it).
+// 2 every k > 8 shape from L = 16 (read per launch, so a test can switch it).  At k <= 8 (X's
+// columns 8 .. 15 zero) it lost to the wide form below L = 64 (profiles/r4u_k8_small_l.txt).
 constexpr int M16_MIN_L = 48;
 static int m16_mode() {
   const char *e = std::getenv("MIGMRES_NT_M16");
@@ -1184,7 +1185,6 @@ static int m16_mode() {
 }
 static bool m16_ok(int L, int k) {
   const int m = m16_mode();
-  if (m == 3 && k >= 2 && k <= 8 && L >= 16 && L < 64) return true;  // k <= 8 below the wide kernels
   return m != 0 && k > 8 && k <= 16 && L >= (m >= 2 ? 16 : M16_MIN_L) && L + 16 <= 512;
 }
 // One instantiation per 16-column step of L; two workgroups per CU (4 waves per SIMD: 128
